@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""Bench of the MI355X ICMP-echo frame transform (BASELINE.json metric).
+
+One step = one pass of the transform (xsk_gpu_echo_dev: parse + full-payload checksums + echo-reply
+rewrite + records + stats counters) over one batch of frames already resident in HBM.  Each step
+gets a fresh, never-transformed batch (a pool of pre-generated batches), so no step sees replies.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4] [--no-cpu] [--host-inclusive]
+
+Multi-GPU: one process per GPU (torch.distributed.run); frame i of a step's global batch goes to
+GPU i mod N (round-robin sharding, no data-path collective); per-GPU work is fixed -> weak scaling.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+CONFIGS = {
+    # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
+    "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
+    "c3": (1 << 20, 1500, 1500, 4096, 0x5EED0003,
+           "c3: 1M x 1500B ICMP echo frames, 4 KiB UMEM-chunk stride, full-payload checksum"),
+    "c4": (1 << 20, 64, 1500, 2048, 0x5EED0004, "c4: 1M x U{64..1500}B ICMP echo frames, 2 KiB stride"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:
+        log(f"warning: --gpus {gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def allreduce(vals, op, world, dev):
+    if world == 1:
+        return vals
+    import torch.distributed as dist
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
+    return t.tolist()
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def cpu_baseline(cfg, budget_s=12.0):
+    """Oracle C port timed on this host's cores on a bounded sample of the same workload."""
+    import oracle
+    n_total, lo, hi, stride, seed, _ = CONFIGS[cfg]
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = min(n_total, 1 << 17)  # 131072 frames
+    umem = np.zeros(n * stride, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi)
+    nbytes = int(descs["len"].sum())
+
+    def run(fn, budget):
+        done, t_tot = 0, 0.0
+        while t_tot < budget:
+            t0 = time.perf_counter()
+            v = fn()
+            t_tot += time.perf_counter() - t0
+            done += n
+            oracle.rearm(umem, descs, v)  # untimed: restore requests for the next pass
+        return done, t_tot
+
+    def full_mt():
+        return oracle.echo_batch(umem, descs, threads=threads)[0]
+
+    def hdr_1t():
+        verd = np.zeros(n, np.uint8)
+        st = np.zeros(1, oracle.STATS_DTYPE)
+        oracle.lib().oracle_echo_batch_hdr(umem.ctypes.data, descs.ctypes.data, n, verd.ctypes.data, st.ctypes.data)
+        return verd
+
+    d1, t1 = run(full_mt, budget_s)
+    d2, t2 = run(hdr_1t, budget_s / 4)
+    return {
+        "value": round(d1 / t1 / 1e6, 3), "unit": "Mframes/s", "cores": threads, "kind": "port",
+        "gib_per_s": round(d1 / n * nbytes / t1 / 2**30, 3),
+        "sample": f"{n} frames of {cfg} ({lo}-{hi} B, stride {stride}), full contract (gates, rewrite, "
+                  f"RFC1071 full-payload sums, records, counters), {threads} pthreads, {t1:.1f} s",
+        "reference_equivalent_1core": {"value": round(d2 / t2 / 1e6, 3), "unit": "Mframes/s", "cores": 1,
+                                       "sample": "header-only transform exactly as process_packet "
+                                                 "(no logging, no sendto, no payload sums)"},
+        "cpu_model": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def traffic_from_profiles(cfg):
+    """PMC-derived HBM bytes per launch, if a committed rocprofv3 --pmc summary exists."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    if os.path.exists(p):
+        try:
+            d = json.load(open(p))
+            return d.get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def host_inclusive(cfg, dev_index):
+    """Rate including PCIe: host UMEM -> staged H2D copy -> kernel -> header write-back -> host."""
+    import oracle
+    import xsknet_amd as X
+    n_total, lo, hi, stride, seed, _ = CONFIGS[cfg]
+    n = min(n_total, 1 << 18)
+    umem = np.zeros(n * stride, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi)
+    out = {}
+    for name, mode in (("staged", X.MODE_STAGED), ("zerocopy", X.MODE_ZEROCOPY)):
+        work = umem.copy()
+        with X.EchoContext(work, dev_index, max_batch=n, mode=mode) as ctx:
+            ctx.process(descs, want_recs=False)  # warm
+            v = None
+            reps, t = 0, 0.0
+            while t < 3.0:
+                oracle.rearm(work, descs, np.zeros(n, np.uint8) if v is None else v)
+                t0 = time.perf_counter()
+                v, _, _ = ctx.process(descs, want_recs=False)
+                t += time.perf_counter() - t0
+                reps += 1
+        out[name] = {"mframes_per_s": round(reps * n / t / 1e6, 3),
+                     "gib_per_s": round(reps * int(descs["len"].sum()) / t / 2**30, 3), "frames_per_call": n}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--host-inclusive", action="store_true", help="also measure the PCIe-inclusive rate")
+    args = ap.parse_args()
+
+    import xsknet_amd as X
+    X.lib()  # fail loudly if the HIP library is missing
+
+    rank, world, local = dist_setup(args.gpus)
+    dev = torch.device("cuda", local)
+    n, lo, hi, stride, seed, desc = CONFIGS[args.config]
+    K, W = args.steps, args.warmup
+
+    # ---- batch pool: one fresh batch per step (generated on the GPU, bit-identical to the oracle) ----
+    batch_bytes = n * stride
+    free, _ = torch.cuda.mem_get_info(dev)
+    per_batch = batch_bytes + n * 16
+    pool = max(1, min(W + K, int(free * 0.85) // per_batch - 1))
+    rearm_in_loop = pool < W + K
+    log(f"[rank {rank}] {desc}; world {world}; pool {pool} batches of {batch_bytes / 2**30:.2f} GiB"
+        + (" (re-arm inside timed loop)" if rearm_in_loop else ""))
+    umems, descss = [], []
+    t0 = time.perf_counter()
+    for b in range(pool):
+        u = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
+        d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        # global frame index of local frame j in batch b: b*n*world + rank + j*world (round robin)
+        X.synth_dev(u, d, n, 0, stride, seed, b * n * world + rank, world, 0, lo, hi)
+        umems.append(u)
+        descss.append(d)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] generated {pool} batches in {time.perf_counter() - t0:.1f} s")
+    frame_bytes = int(descss[0].view(torch.int32).view(-1, 4)[:, 2].to(torch.int64).sum().item())
+
+    verd = torch.empty(n, dtype=torch.uint8, device=dev)
+    recs = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    stats = torch.zeros(40, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(max(16, X.workspace_size(local, n)), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step(s):
+        b = s % pool
+        if rearm_in_loop and s >= pool:
+            X.rearm_dev(umems[b], descss[b], verd, n, stream)  # conservative: counted inside the timing
+        X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream)
+
+    for s in range(W):
+        step(s)
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps between barrier + synchronize ----
+    X.timing_enable(True)
+    barrier(world)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in range(W, W + K):
+        step(s)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    kern_ms, launches = X.timing_read()
+    X.timing_enable(False)
+    wall = t1 - t0
+    ev_ms = ev0.elapsed_time(ev1)
+
+    # ---- correctness of what was timed: every frame of every step accepted and counted ----
+    st = stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    ok = int(st["rx_packets"]) == (W + K) * n and int(st["tx_packets"]) == (W + K) * n
+    vr = verd.cpu().numpy()
+    ok = ok and bool((vr == 0).all())
+    recs_np = recs.cpu().numpy().view(X.REC_DTYPE)
+    ok = ok and bool((recs_np["flags"] == 3).all())
+
+    # read-only streaming ceiling over one batch slab (context for the roofline)
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    X.stream_read_dev(umems[0], batch_bytes, out, stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(5):
+        X.stream_read_dev(umems[0], batch_bytes, out, stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    read_ceiling = batch_bytes * 5 / (e0.elapsed_time(e1) / 1e3) / 1e9
+
+    import torch.distributed as _d  # noqa
+    op_max = _d.ReduceOp.MAX if world > 1 else None
+    op_sum = _d.ReduceOp.SUM if world > 1 else None
+    wall_max, ev_max = allreduce([wall, ev_ms], op_max, world, dev)
+    ok_all, frames_all, bytes_all = allreduce([1.0 if ok else 0.0, float(K * n), float(K * frame_bytes)], op_sum,
+                                              world, dev)
+
+    if rank == 0:
+        value = frames_all / wall_max / 1e6
+        kern_avg_ms = kern_ms / max(launches, 1)
+        achieved = frame_bytes / (kern_avg_ms / 1e3) / 1e9
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mframes/s",
+            "gib_per_s": round(bytes_all / wall_max / 2**30, 2),
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(wall_max / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded counter-based ICMP echo requests generated on-GPU, bit-identical "
+                    "to oracle/echo_oracle.c)",
+            "config": {"workload": desc, "frames_per_gpu": n, "frame_len": [lo, hi], "stride": stride,
+                       "frame_bytes_per_gpu_step": frame_bytes, "parallelism": f"shard{world}:round-robin",
+                       "layout": "device-resident UMEM slab + xdp_desc array",
+                       "rearm_in_timed_region": rearm_in_loop},
+            "verified": bool(ok_all == world),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config),
+                         "kernel": "echo_kernel<4>", "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
+                         "algorithmic_bytes_per_launch": frame_bytes,
+                         "read_ceiling_gbs": round(read_ceiling, 1)},
+            "event_ms_per_step": round(ev_max / K, 4),
+        }
+        if world == 1 and not args.no_cpu:
+            log("[rank 0] CPU baseline ...")
+            res["cpu_baseline"] = cpu_baseline(args.config)
+        if args.host_inclusive and world == 1:
+            log("[rank 0] host-inclusive ...")
+            res["host_inclusive"] = host_inclusive(args.config, local)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

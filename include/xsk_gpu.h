@@ -1,0 +1,189 @@
+/*
+ * xsk_gpu.h — C ABI of the MI355X (gfx950) ICMP-echo frame transform.
+ *
+ * This library replaces the per-descriptor call to the reference's
+ *   static bool process_packet(struct xsk_socket_info*, uint64_t addr, uint32_t len,
+ *                              const struct egress_sock*)          src/lib/xsk_receive.c:113-190
+ * inside the RX batch loop
+ *   for (i = 0; i < rcvd; i++) { ... process_packet(...) ... }     src/lib/xsk_receive.c:220-230
+ * by ONE call per batch of AF_XDP descriptors.  Frames are rewritten in place (echo request ->
+ * echo reply) exactly as the reference does, the per-frame decision comes back as a verdict, and
+ * the four stats counters of `struct stats_record` (src/lib/xsk_utils.h:17-23) are accumulated
+ * exactly as src/lib/xsk_receive.c:171-172,229,233 accumulate them.
+ *
+ * Plain C, no HIP/torch types: streams and device pointers are passed as `void*`.
+ * Every entry point returns 0 or a negative errno value (-EINVAL, -ENOMEM, -EIO, -ENODEV); it never
+ * prints and never exits (the reference logs and `exit()`s; per-frame failures are verdicts here).
+ *
+ * Frame ownership contract (AF_XDP gives every frame its own >= 2048-byte UMEM chunk):
+ *   - the UMEM base is 16-byte aligned and the UMEM size is a multiple of 16;
+ *   - every frame exclusively owns the bytes [addr, addr + max(len, 64)) of the UMEM for the duration
+ *     of a call (frames of one batch never overlap); the library only ever writes bytes
+ *     [addr, addr + 38) of frames whose verdict is XSK_GPU_TX_REPLY, and only reads bytes inside
+ *     [align16(addr), align16(addr) + 64) u [addr, addr + len).
+ */
+#ifndef XSK_GPU_H
+#define XSK_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XSK_GPU_ABI_VERSION 1
+
+/* Descriptors with len above this are DROP_BAD_DESC (AF_XDP frames are <= one UMEM chunk). */
+#define XSK_GPU_MAX_LEN (1u << 30)
+
+/* Frames per wavefront tile == RX_BATCH_SIZE (src/lib/xsk_utils.h:8). */
+#define XSK_GPU_TILE_FRAMES 64
+
+/* One RX descriptor. Binary-identical to `struct xdp_desc` of <linux/if_xdp.h>, which the reference
+ * reads at src/lib/xsk_receive.c:222-223 (addr = UMEM offset, len = frame length). */
+struct xsk_gpu_desc {
+    uint64_t addr;
+    uint32_t len;
+    uint32_t options;
+};
+
+/* Counters. Binary-identical to the reference's `struct stats_record` (src/lib/xsk_utils.h:17-23).
+ * Accumulated, never reset, by every call:
+ *   rx_packets += n                      (xsk_receive.c:233)
+ *   rx_bytes   += sum(len)   all frames  (xsk_receive.c:229)
+ *   tx_packets += #TX_REPLY              (xsk_receive.c:172; the library assumes sendto succeeds)
+ *   tx_bytes   += sum(len)   TX_REPLY    (xsk_receive.c:171)
+ * `timestamp` is never touched (the reference's stats thread owns it, xsk_stats.c:83). */
+struct xsk_gpu_stats {
+    uint64_t timestamp;
+    uint64_t rx_packets;
+    uint64_t rx_bytes;
+    uint64_t tx_packets;
+    uint64_t tx_bytes;
+};
+
+/* Per-frame verdict. The reference returns `false` for every frame (xsk_receive.c:124-146,189);
+ * these codes say WHICH branch it took. */
+enum xsk_gpu_verdict {
+    XSK_GPU_TX_REPLY = 0,       /* gates passed, frame rewritten; the reference sendto()s it (:148-172) */
+    XSK_GPU_DROP_SHORT = 1,     /* len < 20: the three silent length checks (:123-133)               */
+    XSK_GPU_DROP_NOT_IPV4 = 2,  /* bytes 12-13 != 08 00 (:135-138)                                  */
+    XSK_GPU_DROP_NOT_ICMP = 3,  /* byte 23 != 1 (:140-143)                                          */
+    XSK_GPU_DROP_NOT_ECHO = 4,  /* byte 34 != 8 (:144-147)                                          */
+    XSK_GPU_DROP_BAD_DESC = 5   /* build-added: the frame does not lie inside the UMEM, or
+                                   len > XSK_GPU_MAX_LEN (the reference would read out of bounds);
+                                   never emitted for valid descriptors */
+};
+
+/* Record flags (build-added verification of the INPUT frame; the reference never verifies). */
+#define XSK_GPU_F_IP_CSUM_OK 0x01u   /* len >= 34 and the IPv4 header [14,34) sums to 0xFFFF */
+#define XSK_GPU_F_ICMP_CSUM_OK 0x02u /* len >= 42 and the ICMP message [34,len) sums to 0xFFFF */
+
+/* Optional 16-byte per-frame result record. Parsed fields are those the reference reads
+ * (xsk_receive.c:135,140,144,157); they are all zero when len < 20 because the reference reads
+ * nothing then.  Checksums are RFC 1071 folded one's-complement sums of 16-bit big-endian words,
+ * odd tail zero-padded, over the frame's own bytes only (0 for an empty range). */
+struct xsk_gpu_rec {
+    uint8_t verdict;        /* enum xsk_gpu_verdict                                        */
+    uint8_t flags;          /* XSK_GPU_F_*                                                 */
+    uint8_t ip_proto;       /* byte 23                                                     */
+    uint8_t icmp_type;      /* byte 34 as received                                         */
+    uint8_t icmp_code;      /* byte 35                                                     */
+    uint8_t ip_vihl;        /* byte 14 (version/IHL; not checked by the reference)         */
+    uint16_t eth_proto;     /* bytes 12-13, big-endian value                               */
+    uint16_t icmp_csum_in;  /* bytes 36-37 as received, big-endian value                   */
+    uint16_t icmp_csum_out; /* bytes 36-37 after the transform (== in unless TX_REPLY)     */
+    uint16_t ip_sum;        /* folded sum over [14, min(len, 34))                          */
+    uint16_t icmp_sum;      /* folded sum over [34, len)                                   */
+};
+
+/* ------------------------------------------------------------------------------------------ */
+/* Device-resident entry points (frames, descriptors and outputs already in HBM).             */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Bytes of device workspace xsk_gpu_echo_dev() needs for a batch of n frames on `device`
+ * (per-workgroup counter partials; at most 64 KiB). */
+size_t xsk_gpu_workspace_size(int device, uint32_t n);
+
+/* Transform n frames in place on the current HIP device.
+ *   d_umem/umem_size : device UMEM (16-B aligned base, size % 16 == 0)
+ *   d_descs          : n descriptors (device memory, 16-B aligned)
+ *   d_verdicts       : n bytes, or NULL
+ *   d_recs           : n records (16-B aligned), or NULL
+ *   d_stats          : one xsk_gpu_stats in device memory, accumulated; or NULL
+ *   d_workspace      : xsk_gpu_workspace_size() bytes of device memory; may be NULL iff d_stats is
+ *   stream           : hipStream_t (NULL = default stream)
+ * Asynchronous: enqueues the transform kernel (and, with d_stats, a one-workgroup counter fold) on
+ * `stream` and returns.  Replaces xsk_receive.c:220-233 for one batch. */
+int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                     uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
+                     void* d_workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Host-UMEM entry points: the drop-in for the client's RX loop (xsk_receive.c:192-237).       */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct xsk_gpu_ctx xsk_gpu_ctx;
+
+enum xsk_gpu_mode {
+    /* The kernel reads and rewrites the registered host UMEM directly over PCIe (mapped pinned
+     * memory): one launch per batch, no copies of frame bytes.  Best for small RX batches. */
+    XSK_GPU_MODE_ZEROCOPY = 0,
+    /* The frames' UMEM span is copied host->device, transformed in HBM, and the 64-byte header
+     * window of every frame is copied back (strided 2-D copy when the batch has a uniform
+     * stride).  Best for large batches. */
+    XSK_GPU_MODE_STAGED = 1
+};
+
+/* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
+ * xsk_utils.c:132-135).  The UMEM is page-locked (hipHostRegister) until xsk_gpu_fini().
+ * max_batch bounds n of later calls. */
+int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode);
+
+/* Synchronously process one batch of host descriptors against the bound UMEM.  Same outputs as
+ * xsk_gpu_echo_dev(); `verdicts`, `recs` and `stats` are host pointers (each may be NULL). */
+int xsk_gpu_process(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
+                    struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+
+/* Release device buffers and unregister the UMEM. NULL is a no-op. */
+void xsk_gpu_fini(xsk_gpu_ctx* ctx);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Bench / test utilities (not on the hot path).                                               */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Synthetic frame generator, bit-identical to oracle/echo_oracle.c:oracle_synth_frame().
+ * Writes n frames into d_umem at addr = base_off + j*stride and their descriptors into d_descs.
+ * Frame j carries global index first + j*step (round-robin sharding: first = rank, step = world).
+ * mode 0 = valid ICMP echo requests, mode 1 = mixed edge cases / negatives.
+ * len is uniform in [len_lo, len_hi].  Requires base_off % 16 == 0, stride % 16 == 0,
+ * stride >= max(len_hi, 64). */
+int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_descs, uint32_t n,
+                      uint64_t base_off, uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode,
+                      uint32_t len_lo, uint32_t len_hi, void* stream);
+
+/* Re-arm: turn every TX_REPLY frame of a batch back into the echo request it was generated as
+ * (swap fields back, type 0 -> 8, checksum restored).  Used by the bench when it must reuse a batch. */
+int xsk_gpu_rearm_dev(void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts, uint32_t n,
+                      void* stream);
+
+/* Read-only streaming ceiling: sums `bytes` (multiple of 16) of device memory into *d_out (u64).
+ * Used for the measured HBM read ceiling next to the transform. */
+int xsk_gpu_stream_read_dev(const void* d_src, uint64_t bytes, uint64_t* d_out, void* stream);
+
+/* Kernel timing with HIP events recorded around every transform-kernel launch on its own stream
+ * (bench instrumentation).  enable != 0 starts recording (and clears previous samples);
+ * xsk_gpu_timing_read() waits for the recorded launches and returns their summed duration. */
+int xsk_gpu_timing_enable(int enable);
+int xsk_gpu_timing_read(double* total_ms, uint64_t* launches);
+
+/* ABI version and the name of the last HIP error seen by the library (static string). */
+int xsk_gpu_abi_version(void);
+const char* xsk_gpu_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XSK_GPU_H */

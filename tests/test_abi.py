@@ -1,0 +1,133 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every declared symbol,
+and argument validation fails with -EINVAL before touching the device."""
+import ctypes as C
+import errno
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "xsk_gpu.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(xsk_gpu_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = declared_functions()
+    for f in ("xsk_gpu_echo_dev", "xsk_gpu_init", "xsk_gpu_process", "xsk_gpu_fini", "xsk_gpu_workspace_size",
+              "xsk_gpu_synth_dev", "xsk_gpu_rearm_dev", "xsk_gpu_stream_read_dev", "xsk_gpu_abi_version",
+              "xsk_gpu_last_error", "xsk_gpu_timing_enable", "xsk_gpu_timing_read"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    import xsknet_amd as X
+    L = X.lib()
+    for f in declared_functions():
+        assert hasattr(L, f), f
+    out = subprocess.run(["nm", "-D", "--defined-only", X.LIB_PATH], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (xsk_gpu_\w+)", out.stdout))
+    assert set(declared_functions()) <= exported
+
+
+def test_struct_layouts_match_header():
+    import xsknet_amd as X
+    # compile a tiny C probe against the header and compare offsets with the numpy dtypes
+    probe = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "xsk_gpu.h"
+#define O(s,f) printf(#s "." #f " %zu\n", offsetof(struct s, f))
+int main(void){
+ printf("desc %zu rec %zu stats %zu\n", sizeof(struct xsk_gpu_desc), sizeof(struct xsk_gpu_rec), sizeof(struct xsk_gpu_stats));
+ O(xsk_gpu_rec,verdict);O(xsk_gpu_rec,flags);O(xsk_gpu_rec,ip_proto);O(xsk_gpu_rec,icmp_type);O(xsk_gpu_rec,icmp_code);
+ O(xsk_gpu_rec,ip_vihl);O(xsk_gpu_rec,eth_proto);O(xsk_gpu_rec,icmp_csum_in);O(xsk_gpu_rec,icmp_csum_out);
+ O(xsk_gpu_rec,ip_sum);O(xsk_gpu_rec,icmp_sum);
+ O(xsk_gpu_stats,timestamp);O(xsk_gpu_stats,rx_packets);O(xsk_gpu_stats,rx_bytes);O(xsk_gpu_stats,tx_packets);O(xsk_gpu_stats,tx_bytes);
+ O(xsk_gpu_desc,addr);O(xsk_gpu_desc,len);O(xsk_gpu_desc,options);
+ return 0;}
+'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        c = os.path.join(td, "p.c")
+        open(c, "w").write(probe)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", os.path.join(td, "p"), c], check=True)
+        out = subprocess.run([os.path.join(td, "p")], capture_output=True, text=True, check=True).stdout.split("\n")
+    assert out[0] == "desc 16 rec 16 stats 40"
+    offs = dict(line.split() for line in out[1:] if line)
+    for dt, name in ((X.REC_DTYPE, "xsk_gpu_rec"), (X.STATS_DTYPE, "xsk_gpu_stats"), (X.DESC_DTYPE, "xsk_gpu_desc")):
+        for f in dt.names:
+            assert int(offs[f"{name}.{f}"]) == dt.fields[f][1], f
+    # stats_record (reference xsk_utils.h:17-23) and xdp_desc (linux/if_xdp.h) are the same layouts
+    import oracle
+    assert oracle.REC_DTYPE == X.REC_DTYPE and oracle.DESC_DTYPE == X.DESC_DTYPE
+
+
+def test_xdp_desc_binary_compatible():
+    probe = r'''
+#include <linux/if_xdp.h>
+#include <stddef.h>
+#include "xsk_gpu.h"
+_Static_assert(sizeof(struct xdp_desc) == sizeof(struct xsk_gpu_desc), "size");
+_Static_assert(offsetof(struct xdp_desc, len) == offsetof(struct xsk_gpu_desc, len), "len");
+_Static_assert(offsetof(struct xdp_desc, options) == offsetof(struct xsk_gpu_desc, options), "opt");
+int main(void){return 0;}
+'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        c = os.path.join(td, "p.c")
+        open(c, "w").write(probe)
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", os.path.join(td, "p"), c],
+                       check=True)
+
+
+def test_abi_version_and_argument_validation():
+    import xsknet_amd as X
+    L = X.lib()
+    assert L.xsk_gpu_abi_version() == 1
+    EINVAL = -errno.EINVAL
+    # n == 0 is a no-op that touches nothing
+    assert L.xsk_gpu_echo_dev(None, 0, None, 0, None, None, None, None, None) == 0
+    # null / misaligned pointers and sizes are rejected before any HIP call
+    assert L.xsk_gpu_echo_dev(None, 4096, None, 1, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev(0x1001, 4096, 0x2000, 1, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev(0x1000, 4095, 0x2000, 1, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2008, 1, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2000, 1, None, 0x3008, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2000, 1, None, None, 0x4000, None, None) == EINVAL  # stats w/o ws
+    assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 8, 2048, 0, 0, 1, 0, 64, 64, None) == EINVAL
+    assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 32, 0, 0, 1, 0, 64, 64, None) == EINVAL
+    assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 2048, 0, 0, 1, 2, 64, 64, None) == EINVAL
+    assert L.xsk_gpu_stream_read_dev(0x1000, 17, 0x2000, None) == EINVAL
+    ctx = C.c_void_p()
+    buf = np.zeros(64, np.uint8)
+    assert L.xsk_gpu_init(C.byref(ctx), 0, None, 4096, 64, 0) == EINVAL
+    assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data, 4095, 64, 0) == EINVAL
+    assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data, 64, 0, 0) == EINVAL
+    assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data, 64, 64, 7) == EINVAL
+    assert L.xsk_gpu_process(None, None, 0, None, None, None) == EINVAL
+    L.xsk_gpu_fini(None)
+
+
+def test_product_library_does_not_link_the_oracle():
+    import xsknet_amd as X
+    out = subprocess.run(["nm", "-D", X.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "oracle_" not in out
+    ldd = subprocess.run(["ldd", X.LIB_PATH], capture_output=True, text=True).stdout
+    assert "liboracle" not in ldd
+
+
+def test_kernels_are_gfx950_code_objects():
+    """The fat binary embedded in the library carries gfx950 code objects (and only gfx950)."""
+    import xsknet_amd as X
+    blob = open(X.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"amdgcn-amd-amdhsa--gfx942" not in blob and b"amdgcn-amd-amdhsa--gfx90a" not in blob

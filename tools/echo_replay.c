@@ -1,0 +1,107 @@
+/*
+ * echo_replay.c — C driver that replays a UMEM image through the GPU echo transform batch by
+ * batch, the way the reference client's RX loop does (src/lib/xsk_receive.c:192-237), with the
+ * per-descriptor process_packet() call replaced by one xsk_gpu_process() per batch.
+ *
+ *   echo_replay <umem.bin> <descs.bin> <out_umem.bin> <out_verdicts.bin> [batch] [zerocopy|staged]
+ *
+ * umem.bin: raw UMEM bytes (size multiple of 16).  descs.bin: packed struct xdp_desc records
+ * (u64 addr, u32 len, u32 options).  Prints the stats_record counters the reference's stats
+ * thread would print (src/lib/xsk_stats.c:37-68) as one line of key=value pairs.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/xsk_gpu.h"
+
+#define RX_BATCH_SIZE 64 /* src/lib/xsk_utils.h:8 */
+
+static void* slurp(const char* path, size_t* size, size_t align) {
+    FILE* f = fopen(path, "rb");
+    if (!f) return NULL;
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    void* buf = NULL;
+    if (n < 0 || posix_memalign(&buf, align, n > 0 ? (size_t)n : align) != 0) {
+        fclose(f);
+        return NULL;
+    }
+    if (n > 0 && fread(buf, 1, (size_t)n, f) != (size_t)n) {
+        free(buf);
+        fclose(f);
+        return NULL;
+    }
+    fclose(f);
+    *size = (size_t)n;
+    return buf;
+}
+
+static int dump(const char* path, const void* p, size_t n) {
+    FILE* f = fopen(path, "wb");
+    if (!f) return -1;
+    const size_t w = fwrite(p, 1, n, f);
+    fclose(f);
+    return w == n ? 0 : -1;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 5) {
+        fprintf(stderr, "usage: %s umem.bin descs.bin out_umem.bin out_verdicts.bin [batch] [zerocopy|staged]\n",
+                argv[0]);
+        return 2;
+    }
+    const uint32_t batch = argc > 5 ? (uint32_t)strtoul(argv[5], NULL, 10) : RX_BATCH_SIZE;
+    const int mode = (argc > 6 && strcmp(argv[6], "staged") == 0) ? XSK_GPU_MODE_STAGED : XSK_GPU_MODE_ZEROCOPY;
+    size_t umem_size = 0, desc_bytes = 0;
+    /* page-aligned like the reference's posix_memalign(getpagesize(), ...) (xsk_utils.c:135) */
+    uint8_t* umem = (uint8_t*)slurp(argv[1], &umem_size, 4096);
+    struct xsk_gpu_desc* descs = (struct xsk_gpu_desc*)slurp(argv[2], &desc_bytes, 16);
+    if (!umem || !descs || batch == 0) {
+        fprintf(stderr, "cannot read inputs\n");
+        return 1;
+    }
+    const uint32_t n = (uint32_t)(desc_bytes / sizeof *descs);
+    uint8_t* verdicts = (uint8_t*)calloc(n ? n : 1, 1);
+
+    xsk_gpu_ctx* ctx = NULL;
+    int rc = xsk_gpu_init(&ctx, 0, umem, umem_size, batch, mode);
+    if (rc) {
+        fprintf(stderr, "xsk_gpu_init: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
+        return 1;
+    }
+    struct xsk_gpu_stats stats;
+    memset(&stats, 0, sizeof stats);
+    uint64_t freed = 0, tx_ready = 0;
+    /* handle_receive_packets(): one RX peek of <= batch descriptors per iteration */
+    for (uint32_t i = 0; i < n; i += batch) {
+        const uint32_t rcvd = n - i < batch ? n - i : batch;
+        rc = xsk_gpu_process(ctx, descs + i, rcvd, verdicts + i, NULL, &stats);
+        if (rc) {
+            fprintf(stderr, "xsk_gpu_process: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
+            xsk_gpu_fini(ctx);
+            return 1;
+        }
+        /* the reference sendto()s TX_REPLY frames, then frees every frame (:166, :226-227) */
+        for (uint32_t k = 0; k < rcvd; k++) {
+            if (verdicts[i + k] == XSK_GPU_TX_REPLY) tx_ready++;
+            freed++;
+        }
+    }
+    xsk_gpu_fini(ctx);
+    if (dump(argv[3], umem, umem_size) || dump(argv[4], verdicts, n)) {
+        fprintf(stderr, "cannot write outputs\n");
+        return 1;
+    }
+    printf("rx_packets=%llu rx_bytes=%llu tx_packets=%llu tx_bytes=%llu freed=%llu tx_ready=%llu\n",
+           (unsigned long long)stats.rx_packets, (unsigned long long)stats.rx_bytes,
+           (unsigned long long)stats.tx_packets, (unsigned long long)stats.tx_bytes, (unsigned long long)freed,
+           (unsigned long long)tx_ready);
+    free(umem);
+    free(descs);
+    free(verdicts);
+    return 0;
+}

@@ -1,0 +1,188 @@
+"""xsknet_amd — MI355X (gfx950) ICMP-echo frame transform behind a C ABI.
+
+The product is ``libxsknet_amd.so`` (HIP kernels + C host code, see ``include/xsk_gpu.h``).  This
+module is ctypes plumbing so tests and ``bench.py`` can drive that ABI with torch-allocated device
+memory; it contains no compute and has no fallback: if the shared library is missing or cannot be
+loaded, importing the bindings raises.
+
+Reference path replaced: ``process_packet``/``csum_replace2`` in
+``/root/reference/src/lib/xsk_receive.c:101-190`` called per descriptor from the RX batch loop
+``xsk_receive.c:220-233``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno as _errno
+import os
+from typing import Optional
+
+import numpy as np
+
+__all__ = [
+    "LIB_PATH", "lib", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
+    "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
+    "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
+    "MODE_ZEROCOPY", "MODE_STAGED", "timing_enable", "timing_read",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libxsknet_amd.so")
+
+TX_REPLY, DROP_SHORT, DROP_NOT_IPV4, DROP_NOT_ICMP, DROP_NOT_ECHO, DROP_BAD_DESC = range(6)
+VERDICTS = ["TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC"]
+MODE_ZEROCOPY, MODE_STAGED = 0, 1
+
+# struct xsk_gpu_desc == struct xdp_desc (linux/if_xdp.h)
+DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
+# struct xsk_gpu_rec (16 B)
+REC_DTYPE = np.dtype([
+    ("verdict", "u1"), ("flags", "u1"), ("ip_proto", "u1"), ("icmp_type", "u1"),
+    ("icmp_code", "u1"), ("ip_vihl", "u1"), ("eth_proto", "<u2"), ("icmp_csum_in", "<u2"),
+    ("icmp_csum_out", "<u2"), ("ip_sum", "<u2"), ("icmp_sum", "<u2"),
+])
+# struct xsk_gpu_stats == struct stats_record (xsk_utils.h:17-23)
+STATS_DTYPE = np.dtype([("timestamp", "<u8"), ("rx_packets", "<u8"), ("rx_bytes", "<u8"),
+                        ("tx_packets", "<u8"), ("tx_bytes", "<u8")])
+assert DESC_DTYPE.itemsize == 16 and REC_DTYPE.itemsize == 16 and STATS_DTYPE.itemsize == 40
+
+
+class XskGpuError(RuntimeError):
+    def __init__(self, fn: str, rc: int):
+        name = _errno.errorcode.get(-rc, str(rc))
+        detail = ""
+        if _lib is not None:
+            detail = f" (last HIP error: {_lib.xsk_gpu_last_error().decode()})"
+        super().__init__(f"{fn} failed: -{name}{detail}")
+        self.rc = rc
+
+
+_lib: Optional[C.CDLL] = None
+
+_P = C.c_void_p
+_SIGS = {
+    "xsk_gpu_abi_version": ([], C.c_int),
+    "xsk_gpu_last_error": ([], C.c_char_p),
+    "xsk_gpu_workspace_size": ([C.c_int, C.c_uint32], C.c_size_t),
+    "xsk_gpu_echo_dev": ([_P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu_init": ([C.POINTER(_P), C.c_int, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
+    "xsk_gpu_process": ([_P, _P, C.c_uint32, _P, _P, _P], C.c_int),
+    "xsk_gpu_fini": ([_P], None),
+    "xsk_gpu_synth_dev": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                           C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, _P], C.c_int),
+    "xsk_gpu_rearm_dev": ([_P, _P, _P, C.c_uint32, _P], C.c_int),
+    "xsk_gpu_stream_read_dev": ([_P, C.c_uint64, _P, _P], C.c_int),
+    "xsk_gpu_timing_enable": ([C.c_int], C.c_int),
+    "xsk_gpu_timing_read": ([C.POINTER(C.c_double), C.POINTER(C.c_uint64)], C.c_int),
+}
+
+
+def lib() -> C.CDLL:
+    """Load libxsknet_amd.so (raises OSError if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(fn: str, rc: int) -> None:
+    if rc != 0:
+        raise XskGpuError(fn, rc)
+
+
+def _ptr(t) -> Optional[int]:
+    """Device pointer of a torch tensor (or None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+def workspace_size(device: int, n: int) -> int:
+    return int(lib().xsk_gpu_workspace_size(device, n))
+
+
+def echo_dev(umem, descs, n: int, verdicts=None, recs=None, stats=None, workspace=None, stream=None) -> None:
+    """xsk_gpu_echo_dev on torch device tensors (uint8 umem, uint8/int64 views of the structs)."""
+    _check("xsk_gpu_echo_dev", lib().xsk_gpu_echo_dev(
+        _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, _ptr(verdicts), _ptr(recs), _ptr(stats),
+        _ptr(workspace), _stream_ptr(stream)))
+
+
+def synth_dev(umem, descs, n: int, base_off: int, stride: int, seed: int, first: int = 0, step: int = 1,
+              mode: int = 0, len_lo: int = 1500, len_hi: int = 1500, stream=None) -> None:
+    _check("xsk_gpu_synth_dev", lib().xsk_gpu_synth_dev(
+        _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, base_off, stride, seed, first, step, mode,
+        len_lo, len_hi, _stream_ptr(stream)))
+
+
+def rearm_dev(umem, descs, verdicts, n: int, stream=None) -> None:
+    _check("xsk_gpu_rearm_dev", lib().xsk_gpu_rearm_dev(_ptr(umem), _ptr(descs), _ptr(verdicts), n,
+                                                        _stream_ptr(stream)))
+
+
+def stream_read_dev(src, nbytes: int, out, stream=None) -> None:
+    _check("xsk_gpu_stream_read_dev", lib().xsk_gpu_stream_read_dev(_ptr(src), nbytes, _ptr(out),
+                                                                    _stream_ptr(stream)))
+
+
+def timing_enable(on: bool = True) -> None:
+    _check("xsk_gpu_timing_enable", lib().xsk_gpu_timing_enable(1 if on else 0))
+
+
+def timing_read():
+    ms = C.c_double(0.0)
+    cnt = C.c_uint64(0)
+    _check("xsk_gpu_timing_read", lib().xsk_gpu_timing_read(C.byref(ms), C.byref(cnt)))
+    return ms.value, cnt.value
+
+
+class EchoContext:
+    """Host-UMEM drop-in (xsk_gpu_init / xsk_gpu_process / xsk_gpu_fini) over a numpy uint8 UMEM."""
+
+    def __init__(self, umem: np.ndarray, device: int = 0, max_batch: int = 4096, mode: int = MODE_ZEROCOPY):
+        assert umem.dtype == np.uint8 and umem.flags.c_contiguous
+        self.umem = umem
+        self._ctx = C.c_void_p()
+        _check("xsk_gpu_init", lib().xsk_gpu_init(C.byref(self._ctx), device, umem.ctypes.data, umem.nbytes,
+                                                  max_batch, mode))
+
+    def process(self, descs: np.ndarray, want_recs: bool = True):
+        n = len(descs)
+        descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+        verdicts = np.zeros(n, np.uint8)
+        recs = np.zeros(n, REC_DTYPE) if want_recs else None
+        stats = np.zeros(1, STATS_DTYPE)
+        _check("xsk_gpu_process", lib().xsk_gpu_process(
+            self._ctx, descs.ctypes.data, n, verdicts.ctypes.data, recs.ctypes.data if recs is not None else None,
+            stats.ctypes.data))
+        return verdicts, recs, stats[0]
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().xsk_gpu_fini(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,708 @@
+// xsk_echo.hip — gfx950 (MI355X / CDNA4) kernels + C ABI for the ICMP-echo frame transform.
+//
+// Replaces, for a whole batch of AF_XDP descriptors at once, the per-frame call
+//   process_packet()   /root/reference/src/lib/xsk_receive.c:113-190   (gates, field swap, type 8->0,
+//   csum_replace2()    /root/reference/src/lib/xsk_receive.c:101-111    RFC 1624 incremental update)
+// and the counter updates of the batch loop at xsk_receive.c:171-172,229,233.
+//
+// Kernel shape:
+//   * one wavefront owns a 64-frame tile (= RX_BATCH_SIZE, xsk_utils.h:8); lane i owns frame i's
+//     header fields, verdict, record and counters;
+//   * the 64-byte header windows of the tile are loaded with coalesced 16-B loads (4 lanes per frame)
+//     and staged in LDS (80-B padded rows: conflict-free ds_read_b128);
+//   * the rest of every frame (bytes >= 64 of its 16-B aligned window) is streamed by the whole wave
+//     in 1 KiB wave-loads (16 B per lane, nontemporal), P loads kept in flight through a ring over
+//     the tile's flattened chunk list; the full-payload one's-complement sum is accumulated per lane
+//     in 64 bits and reduced across the wave with a shuffle tree, then handed to the owning lane;
+//   * only the 38 header bytes of accepted frames are written back, plus a 16-B record per frame.
+// No MFMA: the op is integer byte arithmetic and HBM-read bound.
+
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "../../include/xsk_gpu.h"
+#include "xsk_echo_kernels.h"
+
+using namespace xskgpu;
+
+namespace {
+
+constexpr int kTile = XSK_GPU_TILE_FRAMES;  // frames per wave tile
+constexpr int kWaves = 4;                   // waves per workgroup
+constexpr int kThreads = kTile * kWaves;    // 256
+constexpr int kRow = 80;                    // LDS bytes per staged header row (64 + 16 pad)
+constexpr int kWin = 64;                    // header window [a16, a16 + 64)
+constexpr int kPrefetch = 4;                // 1 KiB wave-loads in flight per wave
+constexpr uint32_t kMaxLen = 1u << 30;      // build-added descriptor sanity bound (XSK_GPU_MAX_LEN)
+
+struct EchoArgs {
+    uint8_t* umem;
+    uint64_t umem_size;
+    const xsk_gpu_desc* descs;
+    uint32_t n;
+    uint8_t* verdicts;
+    xsk_gpu_rec* recs;
+    unsigned long long* partials;  // [gridDim.x][4]: rx_packets, rx_bytes, tx_packets, tx_bytes
+};
+
+// One slot of the streaming ring.
+struct Slot {
+    u32x4 v;        // 16 payload bytes of this lane
+    uint32_t nv;    // valid bytes of v (0..16)
+    uint32_t frame; // owning frame (lane index in the tile), wave-uniform
+    uint32_t last;  // 1 if this chunk closes its frame, wave-uniform
+};
+
+__device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uint32_t end, uint32_t nch,
+                                            uint32_t a16_lo, uint32_t a16_hi, uint32_t rowhi, const uint8_t* umem,
+                                            uint32_t lane) {
+    s.nv = 0;
+    s.last = 0;
+    s.v = u32x4{0u, 0u, 0u, 0u};
+    if (g >= T) return;  // wave-uniform
+    // chunk g belongs to the first frame whose inclusive chunk-prefix end exceeds g
+    const uint32_t f = (uint32_t)__popcll(__ballot(end <= g));
+    const uint32_t f_end = __builtin_amdgcn_readlane(end, f);
+    const uint32_t f_nch = __builtin_amdgcn_readlane(nch, f);
+    const uint32_t c = g - (f_end - f_nch);
+    const uint64_t base = (((uint64_t)__builtin_amdgcn_readlane(a16_hi, f)) << 32) |
+                          (uint64_t)__builtin_amdgcn_readlane(a16_lo, f);
+    const uint32_t f_rowhi = __builtin_amdgcn_readlane(rowhi, f);
+    const uint32_t blk = (uint32_t)kWin + c * 1024u + lane * 16u;  // row coordinates
+    const int32_t rem = (int32_t)(f_rowhi - blk);
+    s.nv = rem <= 0 ? 0u : (rem >= 16 ? 16u : (uint32_t)rem);
+    s.frame = f;
+    s.last = (c + 1 == f_nch) ? 1u : 0u;
+    if (s.nv) s.v = __builtin_nontemporal_load((const u32x4*)(umem + base + blk));
+}
+
+template <int P>
+__global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kRow];
+    __shared__ unsigned long long s_cnt[kWaves][4];
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    uint8_t* rows = s_hdr[wave];
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t nwaves = gridDim.x * kWaves;
+
+    uint64_t c_rxp = 0, c_rxb = 0, c_txp = 0, c_txb = 0;
+
+    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += nwaves) {
+        // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ------------------------
+        const uint32_t fi = t * kTile + lane;
+        const bool live = fi < a.n;
+        uint64_t addr = 0;
+        uint32_t len = 0;
+        if (live) {
+            const u32x4 d = *(const u32x4*)(a.descs + fi);
+            addr = (uint64_t)d.x | ((uint64_t)d.y << 32);
+            len = d.z;
+        }
+        // build-added bounds check; the reference reads bytes [0,38) whenever len >= 20
+        const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+        const bool ok = live && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+        const bool parse = ok && len >= 20;
+        const uint32_t a16_lo = (uint32_t)addr & ~15u;
+        const uint32_t a16_hi = (uint32_t)(addr >> 32);
+        const uint32_t off = (uint32_t)addr & 15u;
+        // frame end in row coordinates (row 0 = a16); < 2^31 because len <= kMaxLen
+        const uint32_t rowhi = parse ? off + len : 0u;
+        const uint32_t row_need = parse ? min(off + (uint32_t)need, (uint32_t)kWin) : 0u;
+
+        // ---- 2. stage the 64 header windows of the tile in LDS (coalesced: 4 lanes per frame) ------
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = r * 16 + (int)(lane >> 2);
+            const uint32_t k = lane & 3u;
+            const uint32_t f_lo = __shfl(a16_lo, f, 64);
+            const uint32_t f_hi = __shfl(a16_hi, f, 64);
+            const uint32_t f_need = __shfl(row_need, f, 64);
+            u32x4 v = u32x4{0u, 0u, 0u, 0u};
+            if (16u * k < f_need) v = *(const u32x4*)(a.umem + ((((uint64_t)f_hi) << 32) | f_lo) + 16u * k);
+            *(u32x4*)(rows + f * kRow + 16 * (int)k) = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+
+        // ---- 3. streaming chunk list of the tile: bytes [64, rowhi) of each frame, 1 KiB per chunk --
+        const uint32_t nch = rowhi > (uint32_t)kWin ? (rowhi - (uint32_t)kWin + 1023u) >> 10 : 0u;
+        uint32_t end = nch;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(end, o, 64);
+            if (lane >= (uint32_t)o) end += y;
+        }
+        const uint32_t T = __builtin_amdgcn_readlane(end, 63);
+
+        Slot ring[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) issue_chunk(ring[u], (uint32_t)u, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
+
+        // ---- 4. header fields from LDS while the stream is in flight --------------------------------
+        const uint8_t* row = rows + lane * kRow;
+        const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+        const uint32_t sh = off & 3u;
+        uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
+#pragma unroll
+        for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], sh);
+        uint32_t d[16];  // absolute (16-B aligned) dwords of the window
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32x4 x = ((const u32x4*)row)[q];
+            d[4 * q + 0] = x.x;
+            d[4 * q + 1] = x.y;
+            d[4 * q + 2] = x.z;
+            d[4 * q + 3] = x.w;
+        }
+        // one's-complement partials in the absolute-alignment domain (RFC 1071 byte-order rule)
+        const int ip_lo = (int)off + 14;
+        const int ip_hi = parse ? (int)off + (int)min(len, 34u) : ip_lo;
+        const int ic_lo = (int)off + 34;
+        const int ic_hi = parse ? (int)min(rowhi, (uint32_t)kWin) : 0;
+        uint32_t s_ip = 0, s_ic = 0;
+#pragma unroll
+        for (int j = 3; j < 13; ++j) s_ip += halves(keep_bytes(d[j], 4 * j, ip_lo, ip_hi));
+#pragma unroll
+        for (int j = 8; j < 16; ++j) s_ic += halves(keep_bytes(d[j], 4 * j, ic_lo, ic_hi));
+
+        // parsed fields (xsk_receive.c:135,140,144,157)
+        const uint32_t eth_proto = parse ? (((h[3] & 0xFFu) << 8) | ((h[3] >> 8) & 0xFFu)) : 0u;
+        const uint32_t vihl = parse ? (h[3] >> 16) & 0xFFu : 0u;
+        const uint32_t proto = parse ? h[5] >> 24 : 0u;
+        const uint32_t itype = parse ? (h[8] >> 16) & 0xFFu : 0u;
+        const uint32_t icode = parse ? h[8] >> 24 : 0u;
+        const uint32_t csum_le = parse ? h[9] & 0xFFFFu : 0u;  // the reference's uint16_t load (:157)
+
+        uint32_t verdict;
+        if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+        else if (len < 20) verdict = XSK_GPU_DROP_SHORT;           // :123-133
+        else if (eth_proto != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;  // :135
+        else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;     // :140
+        else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;     // :144
+        else verdict = XSK_GPU_TX_REPLY;
+        const bool tx = verdict == XSK_GPU_TX_REPLY;
+
+        // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY), xsk_receive.c:101-111,157
+        uint32_t c16 = (~csum_le) & 0xFFFFu;
+        c16 = (c16 + 0xFFF7u) & 0xFFFFu;  // csum += ~old  (old = 8)
+        c16 += c16 < 0xFFF7u ? 1u : 0u;   // end-around carry
+        // csum += new (new = 0) and its carry test are no-ops
+        const uint32_t csum_new_le = tx ? (~c16) & 0xFFFFu : csum_le;
+
+        // ---- 5. drain the stream: per-lane 64-bit sums, one wave reduction per frame ---------------
+        uint64_t acc = 0;
+        uint32_t sres = 0;  // this lane's frame: stream part of the ICMP sum (absolute domain)
+        for (uint32_t g0 = 0; g0 < T; g0 += P) {
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const uint32_t g = g0 + (uint32_t)u;
+                if (g < T) {
+                    u32x4 v = ring[u].v;
+                    const uint32_t nv = ring[u].nv;
+                    if (nv < 16u) {
+                        v.x = keep_bytes(v.x, 0, 0, (int)nv);
+                        v.y = keep_bytes(v.y, 4, 0, (int)nv);
+                        v.z = keep_bytes(v.z, 8, 0, (int)nv);
+                        v.w = keep_bytes(v.w, 12, 0, (int)nv);
+                    }
+                    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+                    if (ring[u].last) {
+                        const uint32_t tot = wave_sum_u32(fold64(acc));
+                        sres = lane == ring[u].frame ? tot : sres;  // hand the sum to the owning lane
+                        acc = 0;
+                    }
+                }
+                issue_chunk(ring[u], g + (uint32_t)P, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
+            }
+        }
+
+        // ---- 6. checksums of the input frame (build-added verification fields) --------------------
+        const uint32_t odd = (uint32_t)addr & 1u;
+        uint32_t ip_sum = fold32(s_ip);
+        uint32_t ic_sum = fold32(s_ic + sres);
+        if (!odd) {
+            ip_sum = bswap16(ip_sum);
+            ic_sum = bswap16(ic_sum);
+        }
+        uint32_t flags = 0;
+        if (parse && len >= 34 && ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
+        if (parse && len >= 42 && ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
+
+        // ---- 7. echo-reply rewrite, xsk_receive.c:148-157 (bytes 0-11, 26-34, 36-37) -------------
+        if (tx) {
+            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);            // s0 s1 s2 s3
+            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);            // s4 s5 d0 d1
+            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);            // d2 d3 d4 d5
+            const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
+            const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
+            const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
+            uint8_t* pkt = a.umem + addr;
+            if ((addr & 3u) == 0) {
+                uint32_t* p32 = (uint32_t*)pkt;
+                p32[0] = n0;
+                p32[1] = n1;
+                p32[2] = n2;
+                p32[6] = n6;
+                p32[7] = n7;
+                p32[8] = n8;
+                *(uint16_t*)(pkt + 36) = (uint16_t)csum_new_le;
+            } else {
+                const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
+#pragma unroll
+                for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+                for (int b = 0; b < 12; ++b) pkt[24 + b] = (uint8_t)(w[3 + (b >> 2)] >> (8 * (b & 3)));
+                pkt[36] = (uint8_t)csum_new_le;
+                pkt[37] = (uint8_t)(csum_new_le >> 8);
+            }
+        }
+
+        // ---- 8. verdicts, records, counters --------------------------------------------------------
+        if (live) {
+            if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
+            if (a.recs) {
+                u32x4 r;
+                r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+                r.y = icode | (vihl << 8) | (eth_proto << 16);
+                r.z = (parse ? bswap16(csum_le) : 0u) | ((parse ? bswap16(csum_new_le) : 0u) << 16);
+                r.w = (parse ? ip_sum : 0u) | ((parse ? ic_sum : 0u) << 16);
+                ((u32x4*)a.recs)[fi] = r;
+            }
+            c_rxp += 1;
+            c_rxb += len;
+            if (tx) {
+                c_txp += 1;
+                c_txb += len;
+            }
+        }
+    }
+
+    // ---- counters: wave -> workgroup -> one partial row per workgroup (no atomics) -----------------
+    if (a.partials) {
+        c_rxp = wave_sum_u64(c_rxp);
+        c_rxb = wave_sum_u64(c_rxb);
+        c_txp = wave_sum_u64(c_txp);
+        c_txb = wave_sum_u64(c_txb);
+        if (lane == 0) {
+            s_cnt[wave][0] = c_rxp;
+            s_cnt[wave][1] = c_rxb;
+            s_cnt[wave][2] = c_txp;
+            s_cnt[wave][3] = c_txb;
+        }
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            unsigned long long s = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) s += s_cnt[w][threadIdx.x];
+            a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+        }
+    }
+}
+
+// Fold the per-workgroup partials into the caller's stats_record-compatible counters.
+__global__ __launch_bounds__(256) void fold_counters_kernel(const unsigned long long* partials, uint32_t nwg,
+                                                           xsk_gpu_stats* st) {
+    __shared__ unsigned long long s[256];
+    const uint32_t c = threadIdx.x & 3u;
+    unsigned long long acc = 0;
+    for (uint32_t w = threadIdx.x >> 2; w < nwg; w += 64) acc += partials[w * 4 + c];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o >= 4; o >>= 1) {
+        if (threadIdx.x < (uint32_t)o) s[threadIdx.x] += s[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) {
+        unsigned long long* ctr = (unsigned long long*)&st->rx_packets;
+        ctr[threadIdx.x] += s[threadIdx.x];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Synthetic frames: one wave per frame, bit-identical to oracle_synth_frame().
+// ------------------------------------------------------------------------------------------------
+struct SynthArgs {
+    uint8_t* umem;
+    uint64_t umem_size;
+    xsk_gpu_desc* descs;
+    uint32_t n;
+    uint64_t base_off, stride, seed, first, step;
+    int mode;
+    uint32_t len_lo, len_hi;
+};
+
+__device__ __constant__ uint32_t k_short_lens[13] = {0, 1, 13, 14, 19, 20, 21, 33, 34, 37, 38, 41, 42};
+
+__global__ __launch_bounds__(256) void synth_kernel(SynthArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t j = blockIdx.x * 4u + uniform(threadIdx.x >> 6);
+    if (j >= a.n) return;
+    const uint64_t gidx = a.first + (uint64_t)j * a.step;
+    const uint64_t K = mix64(a.seed ^ mix64(gidx));
+    const uint64_t r1 = mix64(K + 1), r2 = mix64(K + 2), r3 = mix64(K + 3), r4 = mix64(K + 4), r5 = mix64(K + 5);
+    uint32_t L = a.len_lo == a.len_hi ? a.len_lo : a.len_lo + (uint32_t)(r5 % (uint64_t)(a.len_hi - a.len_lo + 1));
+    const uint32_t s = a.mode == 1 ? (uint32_t)(r4 >> 32) % 20u : 0u;
+    if (s == 18) L = k_short_lens[(r5 >> 40) % 13];
+    const uint32_t W = L > 64 ? L : 64;
+    const uint64_t addr = a.base_off + (uint64_t)j * a.stride;
+    uint8_t* frame = a.umem + addr;
+
+    // header dwords (little-endian), checksum fields zero for now
+    uint32_t hw[11];
+    const uint32_t eth = s == 6 ? 0x86DDu : s == 7 ? 0x8100u : 0x0800u;
+    const uint32_t vihl = s == 12 ? 0x46u : s == 13 ? 0x65u : 0x45u;
+    const uint32_t tl = (L >= 14 ? L - 14 : 0u) & 0xFFFFu;
+    const uint32_t frag = s == 14 ? 0x2000u : 0x4000u;
+    const uint32_t proto = s == 8 ? 6u : 1u;
+    const uint32_t itype = s == 9 ? 0u : s == 10 ? 13u : 8u;
+    const uint32_t icode = s == 11 ? 5u : 0u;
+    hw[0] = (uint32_t)r1;
+    hw[1] = ((uint32_t)(r1 >> 32) & 0xFFFFu) | ((uint32_t)r2 << 16);
+    hw[2] = (uint32_t)(r2 >> 16);
+    hw[3] = bswap16(eth) | (vihl << 16);
+    hw[4] = bswap16(tl) | ((uint32_t)(r2 >> 48) << 16);
+    hw[5] = bswap16(frag) | (64u << 16) | (proto << 24);
+    hw[6] = (uint32_t)r3 << 16;
+    hw[7] = (uint32_t)(r3 >> 16);
+    hw[8] = (uint32_t)(r3 >> 48) | (itype << 16) | (icode << 24);
+    hw[9] = ((uint32_t)r4 & 0xFFFFu) << 16;
+    hw[10] = ((uint32_t)r4 >> 16) & 0xFFFFu;
+    const bool garbage = s == 19;
+    const bool zero_icmp = s == 17;
+
+    // Build this lane's blocks (<= 4096/16/64 = 4 per lane) and the ICMP partial sum over [34, L).
+    const uint32_t nblk = (W + 15) / 16;
+    u32x4 blk[4];
+    uint32_t s_ic = 0;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const uint32_t b = lane + 64u * (uint32_t)it;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (b < nblk) {
+            const uint64_t p0 = mix64(K + 16 + 2 * (uint64_t)b), p1 = mix64(K + 16 + 2 * (uint64_t)b + 1);
+            uint32_t w[4] = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+            if (!garbage) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t k = 4 * b + (uint32_t)i;  // frame dword index
+                    if (k < 10) w[i] = hw[k];
+                    else if (k == 10) w[i] = (w[i] & 0xFFFF0000u) | hw[10];
+                    if (zero_icmp) {  // bytes [38, L) zero
+                        const int base = 4 * (int)k;
+                        const uint32_t z = keep_bytes(0xFFFFFFFFu, base, 38, (int)L);
+                        w[i] &= ~z;
+                    }
+                    s_ic += halves(keep_bytes(w[i], 4 * (int)k, 34, (int)L));
+                }
+            }
+            v = u32x4{w[0], w[1], w[2], w[3]};
+        }
+        blk[it] = v;
+    }
+    if (!garbage) {
+        const uint32_t tot = wave_sum_u32(s_ic);
+        uint32_t icc = (~bswap16(fold32(tot))) & 0xFFFFu;
+        if (s == 15) icc ^= 0x1234u;
+        uint32_t sip = (hw[3] >> 16) + halves(hw[4]) + halves(hw[5]) + halves(hw[6]) + halves(hw[7]) + (hw[8] & 0xFFFFu);
+        uint32_t ipc = (~bswap16(fold32(sip))) & 0xFFFFu;
+        if (s == 16) ipc ^= 0x5A5Au;
+        // bytes 24-25 live in block 1 (.z low half), bytes 36-37 in block 2 (.y low half); lanes 1, 2
+        if (lane == 1) blk[0].z = (blk[0].z & 0xFFFF0000u) | bswap16(ipc);
+        if (lane == 2) blk[0].y = (blk[0].y & 0xFFFF0000u) | bswap16(icc);
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const uint32_t b = lane + 64u * (uint32_t)it;
+        if (b < nblk) ((u32x4*)frame)[b] = blk[it];
+    }
+    if (lane == 0) {
+        xsk_gpu_desc dd;
+        dd.addr = addr;
+        dd.len = L;
+        dd.options = 0;
+        a.descs[j] = dd;
+    }
+}
+
+// Staged host mode: gather the 38 rewritten header bytes of every TX_REPLY frame into a packed
+// [n][48] array so the host can scatter them back into its UMEM (never touching unowned bytes).
+__global__ __launch_bounds__(256) void pack_headers_kernel(const uint8_t* umem, const xsk_gpu_desc* descs,
+                                                           const uint8_t* verdicts, uint32_t n, uint8_t* pack) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || verdicts[i] != XSK_GPU_TX_REPLY) return;
+    const uint8_t* p = umem + descs[i].addr;
+    uint8_t* q = pack + (uint64_t)i * 48u;
+    for (int k = 0; k < 38; ++k) q[k] = p[k];
+}
+
+// Re-arm TX_REPLY frames (lane per frame, byte granular: bench utility, not the hot path).
+__global__ __launch_bounds__(256) void rearm_kernel(uint8_t* umem, const xsk_gpu_desc* descs, const uint8_t* verdicts,
+                                                    uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || verdicts[i] != XSK_GPU_TX_REPLY) return;
+    uint8_t* p = umem + descs[i].addr;
+    uint8_t t[6];
+    for (int k = 0; k < 6; ++k) t[k] = p[k];
+    for (int k = 0; k < 6; ++k) p[k] = p[6 + k];
+    for (int k = 0; k < 6; ++k) p[6 + k] = t[k];
+    for (int k = 0; k < 4; ++k) {
+        const uint8_t x = p[26 + k];
+        p[26 + k] = p[30 + k];
+        p[30 + k] = x;
+    }
+    p[34] = 8;
+    // csum_replace2(csum, 0, 8) on the LE-loaded field
+    uint32_t c = (uint32_t)p[36] | ((uint32_t)p[37] << 8);
+    uint32_t x = (~c) & 0xFFFFu;
+    x = (x + 0xFFFFu) & 0xFFFFu;
+    x += x < 0xFFFFu ? 1u : 0u;
+    x = (x + 8u) & 0xFFFFu;
+    x += x < 8u ? 1u : 0u;
+    x = (~x) & 0xFFFFu;
+    p[36] = (uint8_t)x;
+    p[37] = (uint8_t)(x >> 8);
+}
+
+// Read-only streaming ceiling: every byte loaded once with 16-B nontemporal loads.
+__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* src, uint64_t nvec, unsigned long long* out) {
+    uint64_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3 * stride < nvec; i += 4 * stride) {
+        const u32x4 a0 = __builtin_nontemporal_load(src + i);
+        const u32x4 a1 = __builtin_nontemporal_load(src + i + stride);
+        const u32x4 a2 = __builtin_nontemporal_load(src + i + 2 * stride);
+        const u32x4 a3 = __builtin_nontemporal_load(src + i + 3 * stride);
+        acc += (uint64_t)a0.x + a0.y + a0.z + a0.w + a1.x + a1.y + a1.z + a1.w;
+        acc += (uint64_t)a2.x + a2.y + a2.z + a2.w + a3.x + a3.y + a3.z + a3.w;
+    }
+    for (; i < nvec; i += stride) {
+        const u32x4 a0 = __builtin_nontemporal_load(src + i);
+        acc += (uint64_t)a0.x + a0.y + a0.z + a0.w;
+    }
+    acc = wave_sum_u64(acc);
+    if ((threadIdx.x & 63u) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------------
+thread_local const char* g_last_error = "ok";
+
+int hip_fail(hipError_t e) {
+    g_last_error = hipGetErrorName(e);
+    return e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
+}
+
+#define HIP_TRY(expr)                              \
+    do {                                           \
+        const hipError_t e__ = (expr);             \
+        if (e__ != hipSuccess) return hip_fail(e__); \
+    } while (0)
+
+constexpr int kMaxDevices = 64;
+struct DevInfo {
+    bool init = false;
+    uint32_t max_wg = 0;  // resident echo workgroups on the whole device
+};
+DevInfo g_dev[kMaxDevices];
+std::mutex g_dev_mu;
+
+int dev_info(int device, DevInfo** out) {
+    if (device < 0 || device >= kMaxDevices) return -ENODEV;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    DevInfo& di = g_dev[device];
+    if (!di.init) {
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        int per_cu = 0;
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        if (cur != device) HIP_TRY(hipSetDevice(device));
+        const hipError_t e =
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&echo_kernel<kPrefetch>),
+                                                         kThreads, 0);
+        if (cur != device) (void)hipSetDevice(cur);
+        if (e != hipSuccess) return hip_fail(e);
+        if (per_cu < 1) per_cu = 1;
+        di.max_wg = (uint32_t)cus * (uint32_t)per_cu;
+        di.init = true;
+    }
+    *out = &di;
+    return 0;
+}
+
+uint32_t echo_grid(const DevInfo* di, uint32_t n) {
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    uint32_t g = (ntiles + kWaves - 1) / kWaves;
+    if (g > di->max_wg) g = di->max_wg;
+    return g < 1 ? 1 : g;
+}
+
+// ---- kernel timing (bench instrumentation) -------------------------------------------------------
+constexpr int kTimerCap = 8192;
+struct Timer {
+    bool on = false;
+    int count = 0;  // recorded pairs since enable
+    hipEvent_t ev[kTimerCap][2];
+    bool created = false;
+    int dev[kTimerCap];
+};
+Timer g_timer;
+std::mutex g_timer_mu;
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+// ================================================================================================
+extern "C" {
+
+int xsk_gpu_abi_version(void) { return XSK_GPU_ABI_VERSION; }
+const char* xsk_gpu_last_error(void) { return g_last_error; }
+
+size_t xsk_gpu_workspace_size(int device, uint32_t n) {
+    DevInfo* di = nullptr;
+    if (dev_info(device, &di) != 0) return 0;
+    return (size_t)echo_grid(di, n) * 4 * sizeof(unsigned long long);
+}
+
+int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                     uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
+                     void* d_workspace, void* stream) {
+    if (n == 0) return 0;
+    if (!d_umem || !d_descs || ((uintptr_t)d_umem & 15u) || (umem_size & 15u) || ((uintptr_t)d_descs & 15u) ||
+        ((uintptr_t)d_recs & 15u))
+        return -EINVAL;
+    if (d_stats && !d_workspace) return -EINVAL;
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    DevInfo* di = nullptr;
+    const int rc = dev_info(device, &di);
+    if (rc) return rc;
+    const uint32_t grid = echo_grid(di, n);
+    hipStream_t s = (hipStream_t)stream;
+    EchoArgs args;
+    args.umem = (uint8_t*)d_umem;
+    args.umem_size = umem_size;
+    args.descs = d_descs;
+    args.n = n;
+    args.verdicts = d_verdicts;
+    args.recs = d_recs;
+    args.partials = d_stats ? (unsigned long long*)d_workspace : nullptr;
+
+    int slot = -1;
+    {
+        std::lock_guard<std::mutex> lk(g_timer_mu);
+        if (g_timer.on && g_timer.count < kTimerCap) {
+            slot = g_timer.count++;
+            g_timer.dev[slot] = device;
+        }
+    }
+    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
+    hipLaunchKernelGGL(echo_kernel<kPrefetch>, dim3(grid), dim3(kThreads), 0, s, args);
+    HIP_TRY(hipGetLastError());
+    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], s));
+    if (d_stats) {
+        hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(256), 0, s, (const unsigned long long*)d_workspace, grid,
+                           d_stats);
+        HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+int xsk_gpu_timing_enable(int enable) {
+    std::lock_guard<std::mutex> lk(g_timer_mu);
+    if (enable && !g_timer.created) {
+        for (int i = 0; i < kTimerCap; ++i) {
+            HIP_TRY(hipEventCreate(&g_timer.ev[i][0]));
+            HIP_TRY(hipEventCreate(&g_timer.ev[i][1]));
+        }
+        g_timer.created = true;
+    }
+    g_timer.on = enable != 0;
+    g_timer.count = 0;
+    return 0;
+}
+
+int xsk_gpu_timing_read(double* total_ms, uint64_t* launches) {
+    std::lock_guard<std::mutex> lk(g_timer_mu);
+    double tot = 0.0;
+    for (int i = 0; i < g_timer.count; ++i) {
+        HIP_TRY(hipEventSynchronize(g_timer.ev[i][1]));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, g_timer.ev[i][0], g_timer.ev[i][1]));
+        tot += ms;
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = (uint64_t)g_timer.count;
+    g_timer.count = 0;
+    return 0;
+}
+
+int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_descs, uint32_t n, uint64_t base_off,
+                      uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode, uint32_t len_lo,
+                      uint32_t len_hi, void* stream) {
+    if (n == 0) return 0;
+    if (!d_umem || !d_descs || (base_off & 15u) || (stride & 15u) || len_lo > len_hi || (mode != 0 && mode != 1) ||
+        ((uintptr_t)d_umem & 15u))
+        return -EINVAL;
+    const uint64_t w = len_hi > 64 ? len_hi : 64;
+    if (stride < w || w > 4096) return -EINVAL;
+    if (base_off + (uint64_t)(n - 1) * stride + w > umem_size) return -EINVAL;
+    SynthArgs a;
+    a.umem = (uint8_t*)d_umem;
+    a.umem_size = umem_size;
+    a.descs = d_descs;
+    a.n = n;
+    a.base_off = base_off;
+    a.stride = stride;
+    a.seed = seed;
+    a.first = first;
+    a.step = step;
+    a.mode = mode;
+    a.len_lo = len_lo;
+    a.len_hi = len_hi;
+    hipLaunchKernelGGL(synth_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int xsk_gpu_rearm_dev(void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts, uint32_t n,
+                      void* stream) {
+    if (n == 0) return 0;
+    if (!d_umem || !d_descs || !d_verdicts) return -EINVAL;
+    hipLaunchKernelGGL(rearm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (uint8_t*)d_umem, d_descs,
+                       d_verdicts, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+// Internal (not in include/xsk_gpu.h): used by the host-UMEM staged mode in xsk_gpu_host.c.
+int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
+                              uint32_t n, uint8_t* d_pack, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(pack_headers_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_umem, d_descs, d_verdicts, n, d_pack);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int xsk_gpu_stream_read_dev(const void* d_src, uint64_t bytes, uint64_t* d_out, void* stream) {
+    if (!d_src || !d_out || (bytes & 15u) || ((uintptr_t)d_src & 15u)) return -EINVAL;
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)cus * 8u), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)d_src, bytes / 16, (unsigned long long*)d_out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"
