@@ -157,8 +157,8 @@ void xsk_gpu_fini(xsk_gpu_ctx* ctx);
  * Writes n frames into d_umem at addr = base_off + j*stride and their descriptors into d_descs.
  * Frame j carries global index first + j*step (round-robin sharding: first = rank, step = world).
  * mode 0 = valid ICMP echo requests, mode 1 = mixed edge cases / negatives.
- * len is uniform in [len_lo, len_hi].  Requires base_off % 16 == 0, stride % 16 == 0,
- * stride >= max(len_hi, 64). */
+ * len is uniform in [len_lo, len_hi]; each frame's chunk is filled for roundup16(max(len, 64))
+ * bytes.  Requires base_off % 16 == 0, stride % 16 == 0, stride >= that extent, extent <= 4096. */
 int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_descs, uint32_t n,
                       uint64_t base_off, uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode,
                       uint32_t len_lo, uint32_t len_hi, void* stream);

@@ -249,7 +249,7 @@ uint32_t oracle_synth_frame(uint64_t seed, uint64_t gidx, int mode, uint32_t len
     uint32_t L = len_lo == len_hi ? len_lo : len_lo + (uint32_t)(r5 % (uint64_t)(len_hi - len_lo + 1));
     const uint32_t s = mode == 1 ? (uint32_t)(r4 >> 32) % 20u : 0u;
     if (s == 18) L = k_short_lens[(r5 >> 40) % 13];
-    const uint32_t W = L > 64 ? L : 64;
+    const uint32_t W = ((L > 64 ? L : 64) + 15u) & ~15u; /* fill extent: whole 16-B blocks */
     if (W > cap) return 0xFFFFFFFFu;
     for (uint32_t o = 0; o < W; o++) out[o] = byte_of(oracle_mix64(K + 16 + (o >> 3)), (int)(o & 7));
     if (s == 19) return L; /* garbage frame: fill pattern only */

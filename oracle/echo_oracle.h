@@ -47,8 +47,8 @@ void oracle_echo_batch_hdr(uint8_t* umem, const struct xsk_gpu_desc* descs, uint
 void oracle_echo_batch_hdr_mt(uint8_t* umem, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                               struct xsk_gpu_stats* stats, int threads);
 
-/* Synthetic frames (bit-identical to xsk_gpu_synth_dev). Writes max(len, 64) bytes to out
- * (cap must be >= that); returns len. */
+/* Synthetic frames (bit-identical to xsk_gpu_synth_dev). Writes roundup16(max(len, 64)) bytes to
+ * out (cap must be >= that); returns len, or 0xFFFFFFFF if it does not fit. */
 uint32_t oracle_synth_frame(uint64_t seed, uint64_t gidx, int mode, uint32_t len_lo, uint32_t len_hi, uint8_t* out,
                             uint32_t cap);
 int oracle_synth_batch(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc* descs, uint32_t n, uint64_t base_off,

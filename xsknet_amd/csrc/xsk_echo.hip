@@ -56,27 +56,44 @@ struct Slot {
     uint32_t last;  // 1 if this chunk closes its frame, wave-uniform
 };
 
+// Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
+constexpr int kRsrcFlags = 0x00020000;
+constexpr int kAuxNT = 2;  // nontemporal: payload bytes are read exactly once
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);  // NB: keep it unsigned (no sign-extension)
+}
+
+// Issue the 16-B load of this lane for chunk g of the tile's flattened chunk list.  Branch-free on
+// the vector side: a raw buffer load whose descriptor (wave-uniform, SGPRs) spans exactly the bytes of
+// the chunk that lie inside the frame, so lanes past the frame end read zeros without touching memory,
+// and nothing forces a wait before the data is consumed P chunks later.
 __device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uint32_t end, uint32_t nch,
                                             uint32_t a16_lo, uint32_t a16_hi, uint32_t rowhi, const uint8_t* umem,
                                             uint32_t lane) {
-    s.nv = 0;
-    s.last = 0;
-    s.v = u32x4{0u, 0u, 0u, 0u};
-    if (g >= T) return;  // wave-uniform
-    // chunk g belongs to the first frame whose inclusive chunk-prefix end exceeds g
-    const uint32_t f = (uint32_t)__popcll(__ballot(end <= g));
-    const uint32_t f_end = __builtin_amdgcn_readlane(end, f);
-    const uint32_t f_nch = __builtin_amdgcn_readlane(nch, f);
-    const uint32_t c = g - (f_end - f_nch);
-    const uint64_t base = (((uint64_t)__builtin_amdgcn_readlane(a16_hi, f)) << 32) |
-                          (uint64_t)__builtin_amdgcn_readlane(a16_lo, f);
-    const uint32_t f_rowhi = __builtin_amdgcn_readlane(rowhi, f);
-    const uint32_t blk = (uint32_t)kWin + c * 1024u + lane * 16u;  // row coordinates
-    const int32_t rem = (int32_t)(f_rowhi - blk);
-    s.nv = rem <= 0 ? 0u : (rem >= 16 ? 16u : (uint32_t)rem);
+    uint32_t f = 0, nrec = 0, last = 0, c = 0, f_rowhi = 0;
+    uint64_t base = 0;
+    if (g < T) {  // wave-uniform
+        // chunk g belongs to the first frame whose inclusive chunk-prefix end exceeds g
+        f = (uint32_t)__popcll(__ballot(end <= g));
+        const uint32_t f_end = rdlane(end, f);
+        const uint32_t f_nch = rdlane(nch, f);
+        c = g - (f_end - f_nch);
+        base = ((uint64_t)rdlane(a16_hi, f) << 32) | (uint64_t)rdlane(a16_lo, f);
+        f_rowhi = rdlane(rowhi, f);
+        const uint32_t cstart = (uint32_t)kWin + c * 1024u;  // row coordinates
+        const uint32_t rem = f_rowhi - cstart;              // > 0 by construction
+        nrec = rem >= 1024u ? 1024u : ((rem + 15u) & ~15u);
+        last = (c + 1 == f_nch) ? 1u : 0u;
+        base += cstart;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(umem + base), (short)0, (int)nrec, kRsrcFlags);
+    s.v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(lane * 16u), 0, kAuxNT);
+    const int32_t rem = (int32_t)(f_rowhi - ((uint32_t)kWin + c * 1024u + lane * 16u));
+    s.nv = g < T ? (rem <= 0 ? 0u : (rem >= 16 ? 16u : (uint32_t)rem)) : 0u;
     s.frame = f;
-    s.last = (c + 1 == f_nch) ? 1u : 0u;
-    if (s.nv) s.v = __builtin_nontemporal_load((const u32x4*)(umem + base + blk));
+    s.last = last;
 }
 
 template <int P>
@@ -96,13 +113,9 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
         // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ------------------------
         const uint32_t fi = t * kTile + lane;
         const bool live = fi < a.n;
-        uint64_t addr = 0;
-        uint32_t len = 0;
-        if (live) {
-            const u32x4 d = *(const u32x4*)(a.descs + fi);
-            addr = (uint64_t)d.x | ((uint64_t)d.y << 32);
-            len = d.z;
-        }
+        const u32x4 dsc = *(const u32x4*)(a.descs + (live ? fi : a.n - 1));  // branch-free, in bounds
+        const uint64_t addr = live ? ((uint64_t)dsc.x | ((uint64_t)dsc.y << 32)) : 0;
+        const uint32_t len = live ? dsc.z : 0u;
         // build-added bounds check; the reference reads bytes [0,38) whenever len >= 20
         const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
         const bool ok = live && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
@@ -115,16 +128,26 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
         const uint32_t row_need = parse ? min(off + (uint32_t)need, (uint32_t)kWin) : 0u;
 
         // ---- 2. stage the 64 header windows of the tile in LDS (coalesced: 4 lanes per frame) ------
+        // all four loads are issued before the first LDS write (unneeded blocks read the UMEM base,
+        // which is always mapped, and are zeroed afterwards: no branch around the load)
+        u32x4 hv[4];
+        bool hneed[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int f = r * 16 + (int)(lane >> 2);
             const uint32_t k = lane & 3u;
-            const uint32_t f_lo = __shfl(a16_lo, f, 64);
-            const uint32_t f_hi = __shfl(a16_hi, f, 64);
-            const uint32_t f_need = __shfl(row_need, f, 64);
-            u32x4 v = u32x4{0u, 0u, 0u, 0u};
-            if (16u * k < f_need) v = *(const u32x4*)(a.umem + ((((uint64_t)f_hi) << 32) | f_lo) + 16u * k);
-            *(u32x4*)(rows + f * kRow + 16 * (int)k) = v;
+            const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
+            const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
+            const uint32_t f_need = (uint32_t)__shfl((int)row_need, f, 64);
+            hneed[r] = 16u * k < f_need;
+            const uint64_t src = hneed[r] ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * k : 0ull;
+            hv[r] = *(const u32x4*)(a.umem + src);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = r * 16 + (int)(lane >> 2);
+            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
+            *(u32x4*)(rows + f * kRow + 16 * (int)(lane & 3u)) = hneed[r] ? hv[r] : z;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -348,7 +371,7 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthArgs a) {
     uint32_t L = a.len_lo == a.len_hi ? a.len_lo : a.len_lo + (uint32_t)(r5 % (uint64_t)(a.len_hi - a.len_lo + 1));
     const uint32_t s = a.mode == 1 ? (uint32_t)(r4 >> 32) % 20u : 0u;
     if (s == 18) L = k_short_lens[(r5 >> 40) % 13];
-    const uint32_t W = L > 64 ? L : 64;
+    const uint32_t W = ((L > 64 ? L : 64) + 15u) & ~15u;  // fill extent: whole 16-B blocks
     const uint64_t addr = a.base_off + (uint64_t)j * a.stride;
     uint8_t* frame = a.umem + addr;
 
@@ -652,7 +675,7 @@ int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_d
     if (!d_umem || !d_descs || (base_off & 15u) || (stride & 15u) || len_lo > len_hi || (mode != 0 && mode != 1) ||
         ((uintptr_t)d_umem & 15u))
         return -EINVAL;
-    const uint64_t w = len_hi > 64 ? len_hi : 64;
+    const uint64_t w = ((len_hi > 64 ? len_hi : 64) + 15u) & ~15ull;
     if (stride < w || w > 4096) return -EINVAL;
     if (base_off + (uint64_t)(n - 1) * stride + w > umem_size) return -EINVAL;
     SynthArgs a;
