@@ -9,6 +9,6 @@ run() { # name timeout cmd...
 rocm-smi --showproductname > gpurun_out/smi.log 2>&1
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-run gputests 900 python -m pytest tests -m gpu -q -x --timeout 600; rc=$?
+run gputests 900 python -m pytest tests -m gpu -q --timeout 600; rc=$?
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 run bench 500 python bench.py --steps 10 --warmup 2 --no-cpu

@@ -33,7 +33,6 @@ namespace {
 constexpr int kTile = XSK_GPU_TILE_FRAMES;  // frames per wave tile
 constexpr int kWaves = 4;                   // waves per workgroup
 constexpr int kThreads = kTile * kWaves;    // 256
-constexpr int kRow = 80;                    // LDS bytes per staged header row (64 + 16 pad)
 constexpr int kWin = 64;                    // header window [a16, a16 + 64)
 constexpr int kPrefetch = 4;                // 1 KiB wave-loads in flight per wave
 constexpr uint32_t kMaxLen = 1u << 30;      // build-added descriptor sanity bound (XSK_GPU_MAX_LEN)
@@ -50,10 +49,10 @@ struct EchoArgs {
 
 // One slot of the streaming ring.
 struct Slot {
-    u32x4 v;        // 16 payload bytes of this lane
-    uint32_t nv;    // valid bytes of v (0..16)
-    uint32_t frame; // owning frame (lane index in the tile), wave-uniform
-    uint32_t last;  // 1 if this chunk closes its frame, wave-uniform
+    u32x4 v;         // 16 payload bytes of this lane
+    uint32_t nv;     // valid bytes of v (0..16)
+    uint32_t frame;  // owning frame (lane index in the tile), wave-uniform
+    uint32_t last;   // 1 if this chunk closes its frame, wave-uniform
 };
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -61,13 +60,27 @@ constexpr int kRsrcFlags = 0x00020000;
 constexpr int kAuxNT = 2;  // nontemporal: payload bytes are read exactly once
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);  // NB: keep it unsigned (no sign-extension)
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);  // keep it unsigned: no sign-extension
+}
+
+// Wave-wide u32 sum with DPP row shifts + row broadcasts (no LDS traffic): after the four row_shr
+// steps lane 15 of each 16-lane row holds the row's inclusive sum; row_bcast:15 and row_bcast:31
+// carry rows 0..2 into lane 63.  Returns the total (wave-uniform, SGPR).
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return rdlane(x, 63);
 }
 
 // Issue the 16-B load of this lane for chunk g of the tile's flattened chunk list.  Branch-free on
 // the vector side: a raw buffer load whose descriptor (wave-uniform, SGPRs) spans exactly the bytes of
 // the chunk that lie inside the frame, so lanes past the frame end read zeros without touching memory,
 // and nothing forces a wait before the data is consumed P chunks later.
+template <int WIN>
 __device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uint32_t end, uint32_t nch,
                                             uint32_t a16_lo, uint32_t a16_hi, uint32_t rowhi, const uint8_t* umem,
                                             uint32_t lane) {
@@ -81,8 +94,8 @@ __device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uin
         c = g - (f_end - f_nch);
         base = ((uint64_t)rdlane(a16_hi, f) << 32) | (uint64_t)rdlane(a16_lo, f);
         f_rowhi = rdlane(rowhi, f);
-        const uint32_t cstart = (uint32_t)kWin + c * 1024u;  // row coordinates
-        const uint32_t rem = f_rowhi - cstart;              // > 0 by construction
+        const uint32_t cstart = (uint32_t)WIN + c * 1024u;  // row coordinates
+        const uint32_t rem = f_rowhi - cstart;             // > 0 by construction
         nrec = rem >= 1024u ? 1024u : ((rem + 15u) & ~15u);
         last = (c + 1 == f_nch) ? 1u : 0u;
         base += cstart;
@@ -90,15 +103,18 @@ __device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uin
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)(umem + base), (short)0, (int)nrec, kRsrcFlags);
     s.v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(lane * 16u), 0, kAuxNT);
-    const int32_t rem = (int32_t)(f_rowhi - ((uint32_t)kWin + c * 1024u + lane * 16u));
+    const int32_t rem = (int32_t)(f_rowhi - ((uint32_t)WIN + c * 1024u + lane * 16u));
     s.nv = g < T ? (rem <= 0 ? 0u : (rem >= 16 ? 16u : (uint32_t)rem)) : 0u;
     s.frame = f;
     s.last = last;
 }
 
-template <int P>
+// P    : 1 KiB wave-loads kept in flight per wave (ring depth)
+// LITE : ablation / layout ceiling — stream every frame byte from offset 0 and sum it, nothing else
+template <int P, bool LITE>
 __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kRow];
+    constexpr int WIN = LITE ? 0 : kWin;
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kWin];
     __shared__ unsigned long long s_cnt[kWaves][4];
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -109,65 +125,100 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
 
     uint64_t c_rxp = 0, c_rxb = 0, c_txp = 0, c_txb = 0;
 
-    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += nwaves) {
+    uint32_t t = blockIdx.x * kWaves + wave;
+    // descriptor of this lane's frame in the first tile (next tiles are prefetched one tile ahead)
+    u32x4 dsc = *(const u32x4*)(a.descs + min(t * kTile + lane, a.n - 1));
+    for (; t < ntiles; t += nwaves) {
         // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ------------------------
         const uint32_t fi = t * kTile + lane;
         const bool live = fi < a.n;
-        const u32x4 dsc = *(const u32x4*)(a.descs + (live ? fi : a.n - 1));  // branch-free, in bounds
         const uint64_t addr = live ? ((uint64_t)dsc.x | ((uint64_t)dsc.y << 32)) : 0;
         const uint32_t len = live ? dsc.z : 0u;
+        {
+            const uint32_t tn = t + nwaves;  // prefetch the next tile's descriptors
+            dsc = *(const u32x4*)(a.descs + min(tn * kTile + lane, a.n - 1));
+        }
         // build-added bounds check; the reference reads bytes [0,38) whenever len >= 20
         const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
         const bool ok = live && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
-        const bool parse = ok && len >= 20;
+        const bool parse = ok && (LITE || len >= 20);
         const uint32_t a16_lo = (uint32_t)addr & ~15u;
         const uint32_t a16_hi = (uint32_t)(addr >> 32);
         const uint32_t off = (uint32_t)addr & 15u;
         // frame end in row coordinates (row 0 = a16); < 2^31 because len <= kMaxLen
         const uint32_t rowhi = parse ? off + len : 0u;
-        const uint32_t row_need = parse ? min(off + (uint32_t)need, (uint32_t)kWin) : 0u;
 
-        // ---- 2. stage the 64 header windows of the tile in LDS (coalesced: 4 lanes per frame) ------
-        // all four loads are issued before the first LDS write (unneeded blocks read the UMEM base,
-        // which is always mapped, and are zeroed afterwards: no branch around the load)
-        u32x4 hv[4];
-        bool hneed[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int f = r * 16 + (int)(lane >> 2);
-            const uint32_t k = lane & 3u;
-            const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
-            const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
-            const uint32_t f_need = (uint32_t)__shfl((int)row_need, f, 64);
-            hneed[r] = 16u * k < f_need;
-            const uint64_t src = hneed[r] ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * k : 0ull;
-            hv[r] = *(const u32x4*)(a.umem + src);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int f = r * 16 + (int)(lane >> 2);
-            const u32x4 z = u32x4{0u, 0u, 0u, 0u};
-            *(u32x4*)(rows + f * kRow + 16 * (int)(lane & 3u)) = hneed[r] ? hv[r] : z;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-
-        // ---- 3. streaming chunk list of the tile: bytes [64, rowhi) of each frame, 1 KiB per chunk --
-        const uint32_t nch = rowhi > (uint32_t)kWin ? (rowhi - (uint32_t)kWin + 1023u) >> 10 : 0u;
+        // ---- 2. streaming chunk list of the tile: bytes [WIN, rowhi) of each frame, 1 KiB chunks ----
+        const uint32_t nch = rowhi > (uint32_t)WIN ? (rowhi - (uint32_t)WIN + 1023u) >> 10 : 0u;
         uint32_t end = nch;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(end, o, 64);
+            const uint32_t y = (uint32_t)__shfl_up((int)end, o, 64);
             if (lane >= (uint32_t)o) end += y;
         }
-        const uint32_t T = __builtin_amdgcn_readlane(end, 63);
-
+        const uint32_t T = rdlane(end, 63);
         Slot ring[P];
 #pragma unroll
-        for (int u = 0; u < P; ++u) issue_chunk(ring[u], (uint32_t)u, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
+        for (int u = 0; u < P; ++u)
+            issue_chunk<WIN>(ring[u], (uint32_t)u, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
 
-        // ---- 4. header fields from LDS while the stream is in flight --------------------------------
-        const uint8_t* row = rows + lane * kRow;
+        // ---- 3. header windows -> LDS by DMA (global_load_lds): 16 frames x 64 B per instruction ----
+        if (!LITE) {
+            const uint32_t row_need = parse ? min(off + (uint32_t)need, (uint32_t)kWin) : 0u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = r * 16 + (int)(lane >> 2);
+                const uint32_t k = lane & 3u;
+                const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
+                const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
+                const uint32_t f_need = (uint32_t)__shfl((int)row_need, f, 64);
+                // unneeded blocks read the (always mapped) UMEM base; those LDS bytes are never used
+                const uint64_t src = 16u * k < f_need ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * k : 0ull;
+                __builtin_amdgcn_global_load_lds((const void*)(a.umem + src),
+                                                 (__attribute__((address_space(3))) void*)(rows + r * 1024), 16, 0, 0);
+            }
+        }
+
+        // ---- 4. drain the stream: per-lane 64-bit sums, one DPP wave reduction per frame ------------
+        uint64_t acc = 0;
+        uint32_t sres = 0;  // this lane's frame: stream part of the ICMP sum (absolute domain)
+        for (uint32_t g0 = 0; g0 < T; g0 += P) {
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const uint32_t g = g0 + (uint32_t)u;
+                if (g < T) {
+                    u32x4 v = ring[u].v;
+                    const uint32_t nv = ring[u].nv;
+                    if (nv < 16u) {
+                        v.x = keep_bytes(v.x, 0, 0, (int)nv);
+                        v.y = keep_bytes(v.y, 4, 0, (int)nv);
+                        v.z = keep_bytes(v.z, 8, 0, (int)nv);
+                        v.w = keep_bytes(v.w, 12, 0, (int)nv);
+                    }
+                    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+                    if (ring[u].last) {
+                        const uint32_t tot = wave_sum_dpp(fold64(acc));
+                        sres = lane == ring[u].frame ? tot : sres;  // hand the sum to the owning lane
+                        acc = 0;
+                    }
+                }
+                issue_chunk<WIN>(ring[u], g + (uint32_t)P, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
+            }
+        }
+
+        if (LITE) {
+            if (live) {
+                c_rxp += 1;
+                c_rxb += len;
+                c_txb += sres;  // keeps the stream live
+            }
+            continue;
+        }
+
+        // ---- 5. header fields from LDS (the DMA is older than every stream load: already landed) ----
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint8_t* row = rows + lane * kWin;
         const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
         const uint32_t sh = off & 3u;
         uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
@@ -203,10 +254,10 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
 
         uint32_t verdict;
         if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
-        else if (len < 20) verdict = XSK_GPU_DROP_SHORT;           // :123-133
+        else if (len < 20) verdict = XSK_GPU_DROP_SHORT;                 // :123-133
         else if (eth_proto != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;  // :135
-        else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;     // :140
-        else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;     // :144
+        else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;           // :140
+        else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;           // :144
         else verdict = XSK_GPU_TX_REPLY;
         const bool tx = verdict == XSK_GPU_TX_REPLY;
 
@@ -216,33 +267,6 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
         c16 += c16 < 0xFFF7u ? 1u : 0u;   // end-around carry
         // csum += new (new = 0) and its carry test are no-ops
         const uint32_t csum_new_le = tx ? (~c16) & 0xFFFFu : csum_le;
-
-        // ---- 5. drain the stream: per-lane 64-bit sums, one wave reduction per frame ---------------
-        uint64_t acc = 0;
-        uint32_t sres = 0;  // this lane's frame: stream part of the ICMP sum (absolute domain)
-        for (uint32_t g0 = 0; g0 < T; g0 += P) {
-#pragma unroll
-            for (int u = 0; u < P; ++u) {
-                const uint32_t g = g0 + (uint32_t)u;
-                if (g < T) {
-                    u32x4 v = ring[u].v;
-                    const uint32_t nv = ring[u].nv;
-                    if (nv < 16u) {
-                        v.x = keep_bytes(v.x, 0, 0, (int)nv);
-                        v.y = keep_bytes(v.y, 4, 0, (int)nv);
-                        v.z = keep_bytes(v.z, 8, 0, (int)nv);
-                        v.w = keep_bytes(v.w, 12, 0, (int)nv);
-                    }
-                    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
-                    if (ring[u].last) {
-                        const uint32_t tot = wave_sum_u32(fold64(acc));
-                        sres = lane == ring[u].frame ? tot : sres;  // hand the sum to the owning lane
-                        acc = 0;
-                    }
-                }
-                issue_chunk(ring[u], g + (uint32_t)P, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
-            }
-        }
 
         // ---- 6. checksums of the input frame (build-added verification fields) --------------------
         const uint32_t odd = (uint32_t)addr & 1u;
@@ -258,9 +282,9 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
 
         // ---- 7. echo-reply rewrite, xsk_receive.c:148-157 (bytes 0-11, 26-34, 36-37) -------------
         if (tx) {
-            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);            // s0 s1 s2 s3
-            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);            // s4 s5 d0 d1
-            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);            // d2 d3 d4 d5
+            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
+            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
+            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
             const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
             const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
             const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
@@ -303,6 +327,7 @@ __global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
                 c_txb += len;
             }
         }
+        __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next tile's DMA
     }
 
     // ---- counters: wave -> workgroup -> one partial row per workgroup (no atomics) -----------------
@@ -548,7 +573,7 @@ int dev_info(int device, DevInfo** out) {
         HIP_TRY(hipGetDevice(&cur));
         if (cur != device) HIP_TRY(hipSetDevice(device));
         const hipError_t e =
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&echo_kernel<kPrefetch>),
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&echo_kernel<kPrefetch, false>),
                                                          kThreads, 0);
         if (cur != device) (void)hipSetDevice(cur);
         if (e != hipSuccess) return hip_fail(e);
@@ -628,7 +653,7 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
         }
     }
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
-    hipLaunchKernelGGL(echo_kernel<kPrefetch>, dim3(grid), dim3(kThreads), 0, s, args);
+    echo_kernel<kPrefetch, false><<<dim3(grid), dim3(kThreads), 0, s>>>(args);
     HIP_TRY(hipGetLastError());
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], s));
     if (d_stats) {
@@ -636,6 +661,48 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
                            d_stats);
         HIP_TRY(hipGetLastError());
     }
+    return 0;
+}
+
+// Internal (not in include/xsk_gpu.h): kernel variants for the tuning sweep in tools/kbench.py.
+//   variant: 0 <P=4>, 1 <P=8>, 2 <P=2>, 3 <P=6>, 10+x = LITE (stream-only ceiling) of the same P
+//   max_grid: 0 = library default, else cap on workgroups
+int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t umem_size,
+                          const struct xsk_gpu_desc* d_descs, uint32_t n, uint8_t* d_verdicts,
+                          struct xsk_gpu_rec* d_recs, void* d_workspace, void* stream) {
+    if (n == 0) return 0;
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    DevInfo* di = nullptr;
+    const int rc = dev_info(device, &di);
+    if (rc) return rc;
+    uint32_t grid = echo_grid(di, n);
+    if (max_grid) {
+        const uint32_t full = ((n + kTile - 1) / kTile + kWaves - 1) / kWaves;
+        grid = max_grid < full ? max_grid : full;
+    }
+    EchoArgs args;
+    args.umem = (uint8_t*)d_umem;
+    args.umem_size = umem_size;
+    args.descs = d_descs;
+    args.n = n;
+    args.verdicts = d_verdicts;
+    args.recs = d_recs;
+    args.partials = (unsigned long long*)d_workspace;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g(grid), b(kThreads);
+    switch (variant) {
+        case 0: echo_kernel<4, false><<<g, b, 0, s>>>(args); break;
+        case 1: echo_kernel<8, false><<<g, b, 0, s>>>(args); break;
+        case 2: echo_kernel<2, false><<<g, b, 0, s>>>(args); break;
+        case 3: echo_kernel<6, false><<<g, b, 0, s>>>(args); break;
+        case 10: echo_kernel<4, true><<<g, b, 0, s>>>(args); break;
+        case 11: echo_kernel<8, true><<<g, b, 0, s>>>(args); break;
+        case 12: echo_kernel<2, true><<<g, b, 0, s>>>(args); break;
+        case 13: echo_kernel<6, true><<<g, b, 0, s>>>(args); break;
+        default: return -EINVAL;
+    }
+    HIP_TRY(hipGetLastError());
     return 0;
 }
 
