@@ -268,7 +268,7 @@ def test_rearm_gpu_roundtrip():
     d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     # valid requests only: mixed-mode frames whose input checksum is 0xFFFF (e.g. len < 34) are not
     # invertible (RFC 1624 maps both 0x0000 and 0xFFFF to 0x0800), so re-arm is exact only on these
-    X.synth_dev(d_umem, d_descs, n, 0, 2048, 77, 0, 1, 0, 20, 1500)
+    X.synth_dev(d_umem, d_descs, n, 0, 2048, 77, 0, 1, 0, 64, 1500)
     before = d_umem.clone()
     d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
     X.echo_dev(d_umem, d_descs, n, d_verd)
@@ -337,7 +337,7 @@ def test_timing_hook():
     assert cnt == 3 and ms > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("grid", [0, 1, 7])
 def test_kernel_variants_parity(variant, grid):
     """Every ring depth / grid shape the tuning sweep may select is bit-exact (multi-tile waves too)."""

@@ -111,8 +111,8 @@ __device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uin
 
 // P    : 1 KiB wave-loads kept in flight per wave (ring depth)
 // LITE : ablation / layout ceiling — stream every frame byte from offset 0 and sum it, nothing else
-template <int P, bool LITE>
-__global__ __launch_bounds__(kThreads) void echo_kernel(EchoArgs a) {
+template <int P, bool LITE, int MINW = 1>
+__global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
     constexpr int WIN = LITE ? 0 : kWin;
     __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kWin];
     __shared__ unsigned long long s_cnt[kWaves][4];
@@ -696,6 +696,9 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         case 1: echo_kernel<8, false><<<g, b, 0, s>>>(args); break;
         case 2: echo_kernel<2, false><<<g, b, 0, s>>>(args); break;
         case 3: echo_kernel<6, false><<<g, b, 0, s>>>(args); break;
+        case 4: echo_kernel<4, false, 8><<<g, b, 0, s>>>(args); break;
+        case 5: echo_kernel<2, false, 8><<<g, b, 0, s>>>(args); break;
+        case 6: echo_kernel<8, false, 6><<<g, b, 0, s>>>(args); break;
         case 10: echo_kernel<4, true><<<g, b, 0, s>>>(args); break;
         case 11: echo_kernel<8, true><<<g, b, 0, s>>>(args); break;
         case 12: echo_kernel<2, true><<<g, b, 0, s>>>(args); break;
