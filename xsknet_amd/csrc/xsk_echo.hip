@@ -111,7 +111,9 @@ __device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uin
 
 // P    : 1 KiB wave-loads kept in flight per wave (ring depth)
 // LITE : ablation / layout ceiling — stream every frame byte from offset 0 and sum it, nothing else
-template <int P, bool LITE, int MINW = 1>
+// ABL (ablation bits, tuning sweep only; 0 in every shipped launch): 1 = skip header write-back,
+// 2 = skip records/verdicts, 4 = skip header DMA (header from stale LDS)
+template <int P, bool LITE, int MINW = 1, int ABL = 0>
 __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
     constexpr int WIN = LITE ? 0 : kWin;
     __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kWin];
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
             issue_chunk<WIN>(ring[u], (uint32_t)u, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
 
         // ---- 3. header windows -> LDS by DMA (global_load_lds): 16 frames x 64 B per instruction ----
-        if (!LITE) {
+        if (!LITE && !(ABL & 4)) {
             const uint32_t row_need = parse ? min(off + (uint32_t)need, (uint32_t)kWin) : 0u;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
         if (parse && len >= 42 && ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
 
         // ---- 7. echo-reply rewrite, xsk_receive.c:148-157 (bytes 0-11, 26-34, 36-37) -------------
-        if (tx) {
+        if (tx && !(ABL & 1)) {
             const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
             const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
             const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
@@ -311,8 +313,8 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
 
         // ---- 8. verdicts, records, counters --------------------------------------------------------
         if (live) {
-            if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
-            if (a.recs) {
+            if (a.verdicts && !(ABL & 2)) a.verdicts[fi] = (uint8_t)verdict;
+            if (a.recs && !(ABL & 2)) {
                 u32x4 r;
                 r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
                 r.y = icode | (vihl << 8) | (eth_proto << 16);
@@ -328,6 +330,383 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
             }
         }
         __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next tile's DMA
+    }
+
+    // ---- counters: wave -> workgroup -> one partial row per workgroup (no atomics) -----------------
+    if (a.partials) {
+        c_rxp = wave_sum_u64(c_rxp);
+        c_rxb = wave_sum_u64(c_rxb);
+        c_txp = wave_sum_u64(c_txp);
+        c_txb = wave_sum_u64(c_txb);
+        if (lane == 0) {
+            s_cnt[wave][0] = c_rxp;
+            s_cnt[wave][1] = c_rxb;
+            s_cnt[wave][2] = c_txp;
+            s_cnt[wave][3] = c_txb;
+        }
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            unsigned long long s = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) s += s_cnt[w][threadIdx.x];
+            a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+        }
+    }
+}
+
+// ================================================================================================
+// v3: continuous ring.  The chunk sequence of a wave runs through all of its tiles without a break:
+// while tile `cur` is drained, tile `nxt` is already described (per-lane metadata, chunk prefix) and
+// its header windows are DMA'd into the other LDS buffer, so the ring keeps issuing nxt's chunks
+// across the boundary and cur's header phase runs with P stream loads still in flight.
+// ================================================================================================
+struct TileLane {       // this lane's frame in one tile
+    uint32_t addr_lo, addr_hi, len;
+    uint32_t rowhi;     // parse ? (addr & 15) + len : 0     (row coordinates, row 0 = addr & ~15)
+    uint32_t nch;       // 1 KiB chunks covering [64, rowhi)
+    uint32_t end;       // inclusive prefix of nch over the tile's 64 lanes
+    uint32_t flags;     // 1 live, 2 ok, 4 parse
+};
+
+__device__ __forceinline__ void make_tile(TileLane& m, uint32_t& T, uint32_t t, const u32x4& dsc, const EchoArgs& a,
+                                          uint32_t lane) {
+    const uint32_t fi = t * kTile + lane;
+    const bool live = fi < a.n;  // false for every lane when t >= ntiles
+    const uint64_t addr = live ? ((uint64_t)dsc.x | ((uint64_t)dsc.y << 32)) : 0;
+    const uint32_t len = live ? dsc.z : 0u;
+    const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+    const bool ok = live && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+    const bool parse = ok && len >= 20;
+    m.addr_lo = (uint32_t)addr;
+    m.addr_hi = (uint32_t)(addr >> 32);
+    m.len = len;
+    m.rowhi = parse ? ((uint32_t)addr & 15u) + len : 0u;
+    m.nch = m.rowhi > (uint32_t)kWin ? (m.rowhi - (uint32_t)kWin + 1023u) >> 10 : 0u;
+    m.flags = (live ? 1u : 0u) | (ok ? 2u : 0u) | (parse ? 4u : 0u);
+    uint32_t end = m.nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)end, o, 64);
+        if (lane >= (uint32_t)o) end += y;
+    }
+    m.end = end;
+    T = rdlane(end, 63);
+}
+
+// One LDS-DMA wave-instruction: 16 B per lane from `src` into LDS [dst, dst + 1 KiB).  Issued from
+// inline asm on purpose: a compiler-visible LDS-DMA in the loop makes LLVM treat vmcnt as out of order
+// and emit vmcnt(0) before every stream-slot use (draining the ring).  Completion is covered by the
+// kernel's own counted s_waitcnt before the header rows are read (§5.7 item 1, M0 saved/restored).
+__device__ __forceinline__ void glds16(const uint8_t* src, uint8_t* dst) {
+    const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)dst;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(uniform(lds))
+        : "memory");
+}
+
+// The tile's 64-byte header windows -> LDS rows (64 B each), 16 frames per DMA instruction.
+__device__ __forceinline__ void dma_headers(const TileLane& m, uint8_t* rows, const EchoArgs& a, uint32_t lane) {
+    const uint32_t need = (m.flags & 4u) ? (m.len > 38 ? m.len : 38u) : 0u;
+    const uint32_t row_need = min((m.addr_lo & 15u) + need, (uint32_t)kWin);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int f = r * 16 + (int)(lane >> 2);
+        const uint32_t k = lane & 3u;
+        const uint32_t f_lo = (uint32_t)__shfl((int)(m.addr_lo & ~15u), f, 64);
+        const uint32_t f_hi = (uint32_t)__shfl((int)m.addr_hi, f, 64);
+        const uint32_t f_need = (uint32_t)__shfl((int)row_need, f, 64);
+        // unneeded blocks read the (always mapped) UMEM base; those LDS bytes are never used
+        const uint64_t src = 16u * k < f_need ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * k : 0ull;
+        glds16(a.umem + src, rows + r * 1024);
+    }
+}
+
+struct Slot3 {
+    u32x4 v;
+    uint32_t nv;     // valid bytes (per lane)
+    uint32_t frame;  // wave-uniform
+    uint32_t flags;  // wave-uniform: 1 = holds a chunk, 2 = chunk closes its frame, 4 = owning tile parity
+};
+
+// Refill a slot with the next issuable chunk position I (in cur = [cs, cs+cT) or nxt = the cT..cT+nT
+// that follow); beyond the described tiles the slot stays empty.  Exactly ONE buffer load is issued
+// either way (an empty slot loads zero bytes), so every refill costs the same vmcnt step and the
+// compiler's wait counting stays exact.
+__device__ __forceinline__ void refill3(Slot3& s, uint32_t& I, uint32_t cs, uint32_t cT, uint32_t nT, uint32_t cpar,
+                                        const TileLane& cur, const TileLane& nxt, const uint8_t* umem,
+                                        uint32_t lane) {
+    uint32_t f = 0, nrec = 0, flags = 0, cstart = 0, f_rowhi = 0;
+    uint64_t base = 0;
+    const uint32_t rel = I - cs;
+    if (rel < cT + nT) {  // wave-uniform
+        const bool in_cur = rel < cT;
+        const uint32_t g = in_cur ? rel : rel - cT;
+        uint32_t f_end, f_nch, lo, hi;
+        if (in_cur) {
+            f = (uint32_t)__popcll(__ballot(cur.end <= g));
+            f_end = rdlane(cur.end, f);
+            f_nch = rdlane(cur.nch, f);
+            lo = rdlane(cur.addr_lo, f);
+            hi = rdlane(cur.addr_hi, f);
+            f_rowhi = rdlane(cur.rowhi, f);
+        } else {
+            f = (uint32_t)__popcll(__ballot(nxt.end <= g));
+            f_end = rdlane(nxt.end, f);
+            f_nch = rdlane(nxt.nch, f);
+            lo = rdlane(nxt.addr_lo, f);
+            hi = rdlane(nxt.addr_hi, f);
+            f_rowhi = rdlane(nxt.rowhi, f);
+        }
+        const uint32_t c = g - (f_end - f_nch);
+        cstart = (uint32_t)kWin + c * 1024u;
+        const uint32_t rem = f_rowhi - cstart;
+        nrec = rem >= 1024u ? 1024u : ((rem + 15u) & ~15u);
+        flags = 1u | ((c + 1 == f_nch) ? 2u : 0u) | ((in_cur ? cpar : cpar ^ 1u) ? 4u : 0u);
+        base = ((((uint64_t)hi) << 32) | (uint64_t)(lo & ~15u)) + cstart;
+        ++I;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(umem + base), (short)0, (int)nrec, kRsrcFlags);
+    s.v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(lane * 16u), 0, kAuxNT);
+    const int32_t rem = (int32_t)(f_rowhi - (cstart + lane * 16u));
+    s.nv = rem <= 0 ? 0u : (rem >= 16 ? 16u : (uint32_t)rem);
+    s.frame = f;
+    s.flags = flags;
+}
+
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+
+// Stores hidden from hipcc's wait-count bookkeeping.  On gfx950 vmcnt retires loads, stores and
+// LDS-DMA in issue order (MI355X_MICROARCH.md, s_waitcnt), but LLVM treats a counter with both loads
+// and stores pending as out-of-order and would drain the whole stream ring (vmcnt(0)) after every
+// header phase.  Nothing in the kernel reads these bytes back, so no wait is needed for them at all;
+// `s_nop 1` ends each statement so the next VALU cannot overwrite the data VGPRs early (§5.7 item 1).
+__device__ __forceinline__ void st_hdr_aligned(uint8_t* p, u32x3 w012, u32x3 w678, uint32_t csum) {
+    asm volatile(
+        "global_store_dwordx3 %0, %1, off\n\t"
+        "global_store_dwordx3 %0, %2, off offset:24\n\t"
+        "global_store_short %0, %3, off offset:36\n\t"
+        "s_nop 1" ::"v"(p),
+        "v"(w012), "v"(w678), "v"(csum)
+        : "memory");
+}
+__device__ __forceinline__ void st_byte(uint8_t* p, uint32_t v) {
+    asm volatile("global_store_byte %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_b128(void* p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 load_desc(const xsk_gpu_desc* d, uint32_t i) {
+    const u32x3 x = *(const u32x3*)(d + i);  // 12 bytes: addr, len (options unused)
+    return u32x4{x.x, x.y, x.z, 0u};
+}
+
+template <int P>
+__global__ __launch_bounds__(kThreads) void echo_kernel3(EchoArgs a) {
+    constexpr uint32_t K = P + 6;  // counted wait: younger VM ops allowed to stay in flight
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][2][kTile * kWin];
+    __shared__ __attribute__((aligned(16))) uint8_t s_dsc[kWaves][kTile * 16];  // prefetched descriptors
+    __shared__ unsigned long long s_cnt[kWaves][4];
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t nw = gridDim.x * kWaves;
+    uint64_t c_rxp = 0, c_rxb = 0, c_txp = 0, c_txb = 0;
+
+    uint32_t tc = blockIdx.x * kWaves + wave;  // cur tile index
+    if (tc < ntiles) {
+        const uint32_t nmax = a.n - 1;
+        const u32x4 d0 = load_desc(a.descs, min(tc * kTile + lane, nmax));
+        const u32x4 d1 = load_desc(a.descs, min((tc + nw) * kTile + lane, nmax));
+        TileLane cur, nxt;
+        uint32_t cT, nT;
+        make_tile(cur, cT, tc, d0, a, lane);
+        dma_headers(cur, s_hdr[wave][0], a, lane);
+        make_tile(nxt, nT, tc + nw, d1, a, lane);
+        if (tc + nw < ntiles) dma_headers(nxt, s_hdr[wave][1], a, lane);
+        // descriptors of the tile after nxt arrive by LDS-DMA (one 1 KiB wave-instruction)
+        glds16((const uint8_t*)(a.descs + min((tc + 2 * nw) * kTile + lane, nmax)), s_dsc[wave]);
+        // VM ops issued after DMA(cur) / DMA(nxt) / the descriptor DMA (stores are not counted: an
+        // undercount only makes the counted waits stricter)
+        uint32_t vm_cur = 4 + 1 + (tc + nw < ntiles ? 4u : 0u);
+        uint32_t vm_nxt = 1;
+        uint32_t vm_dsc = 0;
+        uint32_t cpar = 0;   // parity of cur (selects LDS buffer and stream-sum register)
+        uint32_t cs = 0;     // global chunk position where cur starts
+        uint32_t I = 0;      // next chunk position to issue
+        uint32_t Gc = 0;     // chunks consumed
+        uint32_t sres0 = 0, sres1 = 0;
+        uint64_t acc = 0;
+
+        Slot3 ring[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u) refill3(ring[u], I, cs, cT, nT, cpar, cur, nxt, a.umem, lane);
+        vm_cur += P;
+        vm_nxt += P;
+        vm_dsc += P;
+
+        while (true) {
+            // ---- one round over the ring: consume every slot in issue order, refill it ----
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                if (ring[u].flags & 1u) {
+                    u32x4 v = ring[u].v;
+                    const uint32_t nv = ring[u].nv;
+                    if (nv < 16u) {
+                        v.x = keep_bytes(v.x, 0, 0, (int)nv);
+                        v.y = keep_bytes(v.y, 4, 0, (int)nv);
+                        v.z = keep_bytes(v.z, 8, 0, (int)nv);
+                        v.w = keep_bytes(v.w, 12, 0, (int)nv);
+                    }
+                    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+                    if (ring[u].flags & 2u) {
+                        const uint32_t tot = wave_sum_dpp(fold64(acc));
+                        const bool mine = lane == ring[u].frame;
+                        if (ring[u].flags & 4u) sres1 = mine ? tot : sres1;
+                        else sres0 = mine ? tot : sres0;
+                        acc = 0;
+                    }
+                    ++Gc;
+                }
+                refill3(ring[u], I, cs, cT, nT, cpar, cur, nxt, a.umem, lane);
+            }
+            vm_cur += P;
+            vm_nxt += P;
+            vm_dsc += P;
+
+            // ---- tiles whose chunks are all consumed: header phase, then shift ----
+            while (Gc >= cs + cT && tc < ntiles) {
+                // DMA(cur) must have landed: all but the K youngest VM ops are complete
+                if (vm_cur >= K) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                const uint8_t* row = s_hdr[wave][cpar] + lane * kWin;
+                const uint32_t sres = cpar ? sres1 : sres0;
+                {
+                    const uint32_t flags = cur.flags;
+                    const bool live = flags & 1u, ok = flags & 2u, parse = flags & 4u;
+                    const uint32_t len = cur.len;
+                    const uint32_t off = cur.addr_lo & 15u;
+                    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+                    uint32_t h[10];
+#pragma unroll
+                    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+                    const uint32_t* d = (const uint32_t*)row;
+                    const int ip_lo = (int)off + 14;
+                    const int ip_hi = parse ? (int)off + (int)min(len, 34u) : ip_lo;
+                    const int ic_lo = (int)off + 34;
+                    const int ic_hi = parse ? (int)min(cur.rowhi, (uint32_t)kWin) : 0;
+                    uint32_t s_ip = 0, s_ic = 0;
+#pragma unroll
+                    for (int j = 3; j < 13; ++j) s_ip += halves(keep_bytes(d[j], 4 * j, ip_lo, ip_hi));
+#pragma unroll
+                    for (int j = 8; j < 16; ++j) s_ic += halves(keep_bytes(d[j], 4 * j, ic_lo, ic_hi));
+                    const uint32_t eth_proto = parse ? (((h[3] & 0xFFu) << 8) | ((h[3] >> 8) & 0xFFu)) : 0u;
+                    const uint32_t vihl = parse ? (h[3] >> 16) & 0xFFu : 0u;
+                    const uint32_t proto = parse ? h[5] >> 24 : 0u;
+                    const uint32_t itype = parse ? (h[8] >> 16) & 0xFFu : 0u;
+                    const uint32_t icode = parse ? h[8] >> 24 : 0u;
+                    const uint32_t csum_le = parse ? h[9] & 0xFFFFu : 0u;
+                    uint32_t verdict;
+                    if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+                    else if (len < 20) verdict = XSK_GPU_DROP_SHORT;                 // :123-133
+                    else if (eth_proto != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;  // :135
+                    else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;           // :140
+                    else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;           // :144
+                    else verdict = XSK_GPU_TX_REPLY;
+                    const bool tx = verdict == XSK_GPU_TX_REPLY;
+                    // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY), xsk_receive.c:101-111,157
+                    uint32_t c16 = (~csum_le) & 0xFFFFu;
+                    c16 = (c16 + 0xFFF7u) & 0xFFFFu;
+                    c16 += c16 < 0xFFF7u ? 1u : 0u;
+                    const uint32_t csum_new_le = tx ? (~c16) & 0xFFFFu : csum_le;
+                    uint32_t ip_sum = fold32(s_ip);
+                    uint32_t ic_sum = fold32(s_ic + sres);
+                    if (!(cur.addr_lo & 1u)) {
+                        ip_sum = bswap16(ip_sum);
+                        ic_sum = bswap16(ic_sum);
+                    }
+                    uint32_t rflags = 0;
+                    if (parse && len >= 34 && ip_sum == 0xFFFFu) rflags |= XSK_GPU_F_IP_CSUM_OK;
+                    if (parse && len >= 42 && ic_sum == 0xFFFFu) rflags |= XSK_GPU_F_ICMP_CSUM_OK;
+                    if (tx) {  // xsk_receive.c:148-157
+                        const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);
+                        const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);
+                        const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);
+                        const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);
+                        const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);
+                        const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);
+                        uint8_t* pkt = a.umem + ((((uint64_t)cur.addr_hi) << 32) | (uint64_t)cur.addr_lo);
+                        if ((cur.addr_lo & 3u) == 0) {
+                            st_hdr_aligned(pkt, u32x3{n0, n1, n2}, u32x3{n6, n7, n8}, csum_new_le);
+                        } else {
+                            const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
+#pragma unroll
+                            for (int b = 0; b < 12; ++b) st_byte(pkt + b, w[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+                            for (int b = 0; b < 12; ++b) st_byte(pkt + 24 + b, w[3 + (b >> 2)] >> (8 * (b & 3)));
+                            st_byte(pkt + 36, csum_new_le);
+                            st_byte(pkt + 37, csum_new_le >> 8);
+                        }
+                    }
+                    if (live) {
+                        const uint32_t fi = tc * kTile + lane;
+                        if (a.verdicts) st_byte(a.verdicts + fi, verdict);
+                        if (a.recs) {
+                            u32x4 r;
+                            r.x = verdict | (rflags << 8) | (proto << 16) | (itype << 24);
+                            r.y = icode | (vihl << 8) | (eth_proto << 16);
+                            r.z = (parse ? bswap16(csum_le) : 0u) | ((parse ? bswap16(csum_new_le) : 0u) << 16);
+                            r.w = (parse ? ip_sum : 0u) | ((parse ? ic_sum : 0u) << 16);
+                            st_b128((u32x4*)a.recs + fi, r);
+                        }
+                        c_rxp += 1;
+                        c_rxb += len;
+                        if (tx) {
+                            c_txp += 1;
+                            c_txb += len;
+                        }
+                    }
+                }
+                if (cpar) sres1 = 0;
+                else sres0 = 0;
+                // ---- shift: cur <- nxt, describe the tile after it and start its header DMA ----
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS reads of cur done
+                __builtin_amdgcn_wave_barrier();
+                cs += cT;
+                tc += nw;
+                cur = nxt;
+                cT = nT;
+                cpar ^= 1u;
+                vm_cur = vm_nxt;
+                if (vm_dsc >= K) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                const u32x4 dp = ((const u32x4*)s_dsc[wave])[lane];
+                make_tile(nxt, nT, tc + nw, dp, a, lane);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // descriptor row read before reuse
+                __builtin_amdgcn_wave_barrier();
+                if (tc + nw < ntiles) {
+                    dma_headers(nxt, s_hdr[wave][cpar ^ 1u], a, lane);
+                    vm_cur += 4;
+                    vm_dsc += 4;
+                    vm_nxt = 0;
+                }
+                glds16((const uint8_t*)(a.descs + min((tc + 2 * nw) * kTile + lane, nmax)), s_dsc[wave]);
+                vm_dsc = 0;
+                ++vm_cur;
+                ++vm_nxt;
+            }
+            if (tc >= ntiles) break;
+        }
     }
 
     // ---- counters: wave -> workgroup -> one partial row per workgroup (no atomics) -----------------
@@ -699,6 +1078,14 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         case 4: echo_kernel<4, false, 8><<<g, b, 0, s>>>(args); break;
         case 5: echo_kernel<2, false, 8><<<g, b, 0, s>>>(args); break;
         case 6: echo_kernel<8, false, 6><<<g, b, 0, s>>>(args); break;
+        case 21: echo_kernel<4, false, 1, 1><<<g, b, 0, s>>>(args); break;
+        case 22: echo_kernel<4, false, 1, 2><<<g, b, 0, s>>>(args); break;
+        case 24: echo_kernel<4, false, 1, 4><<<g, b, 0, s>>>(args); break;
+        case 27: echo_kernel<4, false, 1, 7><<<g, b, 0, s>>>(args); break;
+        case 30: echo_kernel3<4><<<g, b, 0, s>>>(args); break;
+        case 31: echo_kernel3<8><<<g, b, 0, s>>>(args); break;
+        case 32: echo_kernel3<2><<<g, b, 0, s>>>(args); break;
+        case 33: echo_kernel3<6><<<g, b, 0, s>>>(args); break;
         case 10: echo_kernel<4, true><<<g, b, 0, s>>>(args); break;
         case 11: echo_kernel<8, true><<<g, b, 0, s>>>(args); break;
         case 12: echo_kernel<2, true><<<g, b, 0, s>>>(args); break;
