@@ -731,6 +731,367 @@ __global__ __launch_bounds__(kThreads) void echo_kernel3(EchoArgs a) {
     }
 }
 
+// ================================================================================================
+// v4: row streaming.  The wave still owns a 64-frame tile (lane f = frame f for descriptor, header,
+// verdict, record and counters), but the payload is streamed by the four 16-lane DPP rows of the
+// wave: in step s, row q streams frame 4s+q with 256-B row-loads (16 B per lane), so a 1500-B frame
+// takes 6 loads at 98 % lane utilisation and its partial sum is folded inside the row by 4 DPP row
+// shifts instead of a whole-wave reduction.  Latency is hidden by occupancy (<= 64 VGPRs, 8 waves
+// per SIMD) plus U loads in flight per lane, not by a cross-frame ring.
+// ================================================================================================
+__device__ __forceinline__ uint32_t row_sum_dpp(uint32_t x) {  // lane 15 of each 16-lane row: row total
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    return x;
+}
+
+// Mask keeping the low nb bytes of a dword (nb <= 0: none, nb >= 4: all).
+__device__ __forceinline__ uint32_t dw_mask(int nb) {
+    return nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+}
+
+// One frame's header work (lane = frame): gates, rewrite, checksums, verdict, record, counters.
+// `row` is the frame's 64-B header window [a16, a16 + 64) in LDS; `sres` the folded stream sum of
+// row bytes [64, rowhi) in the absolute-alignment domain.
+struct Counters {
+    uint64_t rxp = 0, rxb = 0, txp = 0, txb = 0;
+};
+
+// WB64: a 16-B aligned reply is patched into its LDS row instead of memory and the function returns
+// true; the caller then stores the whole 64-B window with coalesced full-sector writes (bytes other
+// than [0,38) are rewritten with the values they held).  Unaligned replies are stored byte-exact here.
+template <bool WB64>
+__device__ __forceinline__ bool header_phase(const EchoArgs& a, uint8_t* row, uint32_t sres, uint64_t addr,
+                                             uint32_t len, bool live, bool ok, bool parse, uint32_t fi,
+                                             Counters& cnt) {
+    const uint32_t off = (uint32_t)addr & 15u;
+    const uint32_t rowhi = parse ? off + len : 0u;
+    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+    uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+    uint32_t d[16];  // absolute (16-B aligned) dwords of the window
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const u32x4 x = ((const u32x4*)row)[q];
+        d[4 * q + 0] = x.x;
+        d[4 * q + 1] = x.y;
+        d[4 * q + 2] = x.z;
+        d[4 * q + 3] = x.w;
+    }
+    const int ip_lo = (int)off + 14;
+    const int ip_hi = parse ? (int)off + (int)min(len, 34u) : ip_lo;
+    const int ic_lo = (int)off + 34;
+    const int ic_hi = parse ? (int)min(rowhi, (uint32_t)kWin) : 0;
+    uint32_t s_ip = 0, s_ic = 0;
+#pragma unroll
+    for (int j = 3; j < 13; ++j) s_ip += halves(keep_bytes(d[j], 4 * j, ip_lo, ip_hi));
+#pragma unroll
+    for (int j = 8; j < 16; ++j) s_ic += halves(keep_bytes(d[j], 4 * j, ic_lo, ic_hi));
+
+    // parsed fields (xsk_receive.c:135,140,144,157)
+    const uint32_t eth_proto = parse ? (((h[3] & 0xFFu) << 8) | ((h[3] >> 8) & 0xFFu)) : 0u;
+    const uint32_t vihl = parse ? (h[3] >> 16) & 0xFFu : 0u;
+    const uint32_t proto = parse ? h[5] >> 24 : 0u;
+    const uint32_t itype = parse ? (h[8] >> 16) & 0xFFu : 0u;
+    const uint32_t icode = parse ? h[8] >> 24 : 0u;
+    const uint32_t csum_le = parse ? h[9] & 0xFFFFu : 0u;  // the reference's uint16_t load (:157)
+
+    uint32_t verdict;
+    if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+    else if (len < 20) verdict = XSK_GPU_DROP_SHORT;                 // :123-133
+    else if (eth_proto != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;  // :135
+    else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;           // :140
+    else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;           // :144
+    else verdict = XSK_GPU_TX_REPLY;
+    const bool tx = verdict == XSK_GPU_TX_REPLY;
+
+    // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY), xsk_receive.c:101-111,157
+    uint32_t c16 = (~csum_le) & 0xFFFFu;
+    c16 = (c16 + 0xFFF7u) & 0xFFFFu;  // csum += ~old  (old = 8)
+    c16 += c16 < 0xFFF7u ? 1u : 0u;   // end-around carry; csum += new (0) is a no-op
+    const uint32_t csum_new_le = tx ? (~c16) & 0xFFFFu : csum_le;
+
+    // RFC 1071 sums of the input frame (build-added verification fields)
+    uint32_t ip_sum = fold32(s_ip);
+    uint32_t ic_sum = fold32(s_ic + sres);
+    if (!((uint32_t)addr & 1u)) {
+        ip_sum = bswap16(ip_sum);
+        ic_sum = bswap16(ic_sum);
+    }
+    uint32_t flags = 0;
+    if (parse && len >= 34 && ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
+    if (parse && len >= 42 && ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
+
+    // echo-reply rewrite, xsk_receive.c:148-157 (bytes 0-11, 26-34, 36-37)
+    bool wb = false;
+    if (tx) {
+        const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
+        const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
+        const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
+        const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
+        const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
+        const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
+        uint8_t* pkt = a.umem + addr;
+        if (WB64 && (addr & 15u) == 0 && a.umem_size - addr >= (uint64_t)kWin) {
+            uint32_t* r32 = (uint32_t*)row;  // row 0 == frame byte 0
+            r32[0] = n0;
+            r32[1] = n1;
+            r32[2] = n2;
+            r32[6] = n6;
+            r32[7] = n7;
+            r32[8] = n8;
+            r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+            wb = true;
+        } else if ((addr & 3u) == 0) {
+            uint32_t* p32 = (uint32_t*)pkt;
+            p32[0] = n0;
+            p32[1] = n1;
+            p32[2] = n2;
+            p32[6] = n6;
+            p32[7] = n7;
+            p32[8] = n8;
+            *(uint16_t*)(pkt + 36) = (uint16_t)csum_new_le;
+        } else {
+            const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
+#pragma unroll
+            for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+            for (int b = 0; b < 12; ++b) pkt[24 + b] = (uint8_t)(w[3 + (b >> 2)] >> (8 * (b & 3)));
+            pkt[36] = (uint8_t)csum_new_le;
+            pkt[37] = (uint8_t)(csum_new_le >> 8);
+        }
+    }
+    if (live) {
+        if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
+        if (a.recs) {
+            u32x4 r;
+            r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+            r.y = icode | (vihl << 8) | (eth_proto << 16);
+            r.z = (parse ? bswap16(csum_le) : 0u) | ((parse ? bswap16(csum_new_le) : 0u) << 16);
+            r.w = (parse ? ip_sum : 0u) | ((parse ? ic_sum : 0u) << 16);
+            ((u32x4*)a.recs)[fi] = r;
+        }
+        cnt.rxp += 1;
+        cnt.rxb += len;
+        if (tx) {
+            cnt.txp += 1;
+            cnt.txb += len;
+        }
+    }
+    return wb;
+}
+
+// Counters: wave -> workgroup -> one partial row per workgroup (no atomics).
+__device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, unsigned long long (*s_cnt)[4],
+                                               uint32_t wave, uint32_t lane) {
+    if (!a.partials) return;
+    c.rxp = wave_sum_u64(c.rxp);
+    c.rxb = wave_sum_u64(c.rxb);
+    c.txp = wave_sum_u64(c.txp);
+    c.txb = wave_sum_u64(c.txb);
+    if (lane == 0) {
+        s_cnt[wave][0] = c.rxp;
+        s_cnt[wave][1] = c.rxb;
+        s_cnt[wave][2] = c.txp;
+        s_cnt[wave][3] = c.txb;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long s = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) s += s_cnt[w][threadIdx.x];
+        a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {  // uniform result (SGPRs)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    return ((uint64_t)uniform((uint32_t)(x >> 32)) << 32) | (uint64_t)uniform((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o, 64);
+        x = y > x ? y : x;
+    }
+    return ((uint64_t)uniform((uint32_t)(x >> 32)) << 32) | (uint64_t)uniform((uint32_t)x);
+}
+
+// Stream loaders: `in` = the block lies (at least partly) inside the lane's frame.
+struct WinLoader {  // tile-wide buffer window; out-of-range offsets return zeros, no memory access
+    static constexpr bool kZeroFill = true;
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t rel;  // frame's a16 relative to the window base
+    __device__ __forceinline__ u32x4 load(uint32_t ro, bool in) const {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(in ? rel + ro : 0x80000000u), 0, kAuxNT);
+    }
+};
+struct FarLoader {  // 64-bit addresses; lanes past the frame re-read its first block (masked to zero)
+    static constexpr bool kZeroFill = false;
+    const uint8_t* fbase;
+    __device__ __forceinline__ u32x4 load(uint32_t ro, bool in) const {
+        return __builtin_nontemporal_load((const u32x4*)(fbase + (in ? ro : 0u)));
+    }
+};
+
+// Sum (64-bit, of LE dwords) of row bytes [64, f_rowhi) of this lane's frame: lane k of the row takes
+// bytes [64 + 256 j + 16 k, +16) for j < ns.  U loads are issued before the first is consumed.
+template <int U, class L>
+__device__ __forceinline__ uint64_t stream_row(const L& ld, uint32_t ns, uint32_t f_rowhi, uint32_t k) {
+    uint64_t acc = 0;
+    for (uint32_t j0 = 0; j0 < ns; j0 += U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = (uint32_t)kWin + 256u * (j0 + (uint32_t)u) + 16u * k;
+            v[u] = ld.load(ro, ro < f_rowhi);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = (uint32_t)kWin + 256u * (j0 + (uint32_t)u) + 16u * k;
+            const int nb = (int)(f_rowhi - min(ro, f_rowhi));  // valid bytes of this block (0..)
+            u32x4 x = v[u];
+            const bool fix = L::kZeroFill ? (nb > 0 && nb < 16) : (nb < 16);
+            if (__ballot(fix) != 0ull) {  // wave-uniform: only blocks that end (or miss) a frame
+                x.x &= dw_mask(nb);
+                x.y &= dw_mask(nb - 4);
+                x.z &= dw_mask(nb - 8);
+                x.w &= dw_mask(nb - 12);
+            }
+            acc += (uint64_t)x.x + (uint64_t)x.y + (uint64_t)x.z + (uint64_t)x.w;
+        }
+    }
+    return acc;
+}
+
+template <int U, int MINW, bool WB64 = true>
+__global__ __launch_bounds__(kThreads, MINW) void echo_kernel4(EchoArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kWin];
+    __shared__ uint32_t s_sum[kWaves][kTile];
+    __shared__ unsigned long long s_cnt[kWaves][4];
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    uint8_t* rows = s_hdr[wave];
+    uint32_t* sums = s_sum[wave];
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t nwaves = gridDim.x * kWaves;
+    Counters cnt;
+
+    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += nwaves) {
+        // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------------
+        const uint32_t fi = t * kTile + lane;
+        const bool live = fi < a.n;
+        u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
+        if (live) dsc = *(const u32x4*)(a.descs + fi);
+        const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
+        const uint32_t len = dsc.z;
+        // build-added bounds check; the reference reads bytes [0,38) whenever len >= 20
+        const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+        const bool ok = live && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+        const bool parse = ok && len >= 20;
+        const uint32_t off = (uint32_t)addr & 15u;
+        const uint32_t a16_lo = (uint32_t)addr & ~15u;
+        const uint32_t a16_hi = (uint32_t)(addr >> 32);
+        const uint32_t rowhi = parse ? off + len : 0u;  // frame end, row coordinates (row 0 = a16)
+
+        // ---- 2. header windows -> LDS by DMA: 16 frames x 64 B per wave-instruction -----------------
+        {
+            // the whole window when it lies in the UMEM (the write-back of step 5 stores all of it)
+            const uint64_t room = a.umem_size - (addr & ~15ull);
+            const uint32_t row_need = parse ? (uint32_t)min(room, (uint64_t)kWin) : 0u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = r * 16 + (int)(lane >> 2);
+                const uint32_t kk = lane & 3u;
+                const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
+                const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
+                const uint32_t f_need = (uint32_t)__shfl((int)row_need, f, 64);
+                // unneeded blocks read the (always mapped) UMEM base; those LDS bytes are never used
+                const uint64_t src =
+                    16u * kk < f_need ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * kk : 0ull;
+                glds16(a.umem + src, rows + r * 1024);  // asm: keeps LLVM's vmcnt bookkeeping in order
+            }
+        }
+
+        // ---- 3. stream row bytes [64, rowhi): row q of step s owns frame 4s+q -----------------------
+        const uint32_t nit = rowhi > (uint32_t)kWin ? (rowhi - (uint32_t)kWin + 255u) >> 8 : 0u;
+        if (__ballot(nit != 0u) != 0ull) {
+            // one buffer window [wlo, whi) over every streamed byte of the tile; lanes past their
+            // frame's end get an out-of-range offset and load zeros without touching memory
+            const uint64_t a16 = addr & ~15ull;
+            const uint64_t wlo = wave_min_u64(nit ? a16 : ~0ull);
+            const uint64_t whi = wave_max_u64(nit ? addr + len : 0ull);
+            const uint64_t span = (whi - wlo + 15u) & ~15ull;  // <= umem_size - wlo (size % 16 == 0)
+            if (span < 0x80000000ull) {
+                WinLoader ld;
+                ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + wlo), (short)0, (int)span, kRsrcFlags);
+                const uint32_t rel = nit ? (uint32_t)(a16 - wlo) : 0u;
+                for (uint32_t s = 0; s < 16; ++s) {
+                    const int f = (int)(4u * s + q);
+                    const uint32_t f_nit = (uint32_t)__shfl((int)nit, f, 64);
+                    const uint32_t ns = max(max(rdlane(f_nit, 0), rdlane(f_nit, 16)), max(rdlane(f_nit, 32), rdlane(f_nit, 48)));
+                    if (ns == 0) continue;
+                    ld.rel = (uint32_t)__shfl((int)rel, f, 64);
+                    const uint32_t f_rowhi = (uint32_t)__shfl((int)rowhi, f, 64);
+                    const uint32_t r = row_sum_dpp(fold64(stream_row<U>(ld, ns, f_rowhi, k)));
+                    if (k == 15u) sums[f] = r;
+                }
+            } else {  // frames of one tile more than 2 GiB apart: 64-bit addresses, clamped loads
+                for (uint32_t s = 0; s < 16; ++s) {
+                    const int f = (int)(4u * s + q);
+                    const uint32_t f_nit = (uint32_t)__shfl((int)nit, f, 64);
+                    const uint32_t ns = max(max(rdlane(f_nit, 0), rdlane(f_nit, 16)), max(rdlane(f_nit, 32), rdlane(f_nit, 48)));
+                    if (ns == 0) continue;
+                    const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
+                    const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
+                    FarLoader ld;
+                    ld.fbase = a.umem + (f_nit ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) : 0ull);
+                    const uint32_t f_rowhi = (uint32_t)__shfl((int)rowhi, f, 64);
+                    const uint32_t r = row_sum_dpp(fold64(stream_row<U>(ld, ns, f_rowhi, k)));
+                    if (k == 15u) sums[f] = r;
+                }
+            }
+        }
+
+        // ---- 4. header phase (lane = frame); the DMA is older than every stream load --------------
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t sres = nit ? sums[lane] : 0u;
+        const bool wb = header_phase<WB64>(a, rows + lane * kWin, sres, addr, len, live, ok, parse, fi, cnt);
+        if (WB64) {
+            // ---- 5. patched windows -> UMEM: 16 frames x 64 B per wave-store, whole 64-B sectors ----
+            const uint64_t wbm = __ballot(wb);
+            if (wbm) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int f = r * 16 + (int)(lane >> 2);
+                    const uint32_t kk = lane & 3u;
+                    const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
+                    const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
+                    if ((wbm >> f) & 1ull) {
+                        const u32x4 w = *(const u32x4*)(rows + f * kWin + 16u * kk);
+                        *(u32x4*)(a.umem + ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * kk) = w;
+                    }
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next tile's DMA
+    }
+    store_partials(a, cnt, s_cnt, wave, lane);
+}
+
 // Fold the per-workgroup partials into the caller's stats_record-compatible counters.
 __global__ __launch_bounds__(256) void fold_counters_kernel(const unsigned long long* partials, uint32_t nwg,
                                                            xsk_gpu_stats* st) {
@@ -1086,6 +1447,12 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         case 31: echo_kernel3<8><<<g, b, 0, s>>>(args); break;
         case 32: echo_kernel3<2><<<g, b, 0, s>>>(args); break;
         case 33: echo_kernel3<6><<<g, b, 0, s>>>(args); break;
+        case 40: echo_kernel4<6, 1><<<g, b, 0, s>>>(args); break;
+        case 41: echo_kernel4<6, 8><<<g, b, 0, s>>>(args); break;
+        case 42: echo_kernel4<3, 8><<<g, b, 0, s>>>(args); break;
+        case 43: echo_kernel4<6, 6><<<g, b, 0, s>>>(args); break;
+        case 44: echo_kernel4<4, 8><<<g, b, 0, s>>>(args); break;
+        case 45: echo_kernel4<6, 1, false><<<g, b, 0, s>>>(args); break;
         case 10: echo_kernel<4, true><<<g, b, 0, s>>>(args); break;
         case 11: echo_kernel<8, true><<<g, b, 0, s>>>(args); break;
         case 12: echo_kernel<2, true><<<g, b, 0, s>>>(args); break;
