@@ -169,6 +169,7 @@ def main():
     args = ap.parse_args()
 
     import xsknet_amd as X
+    from xsknet_amd import shard
     X.lib()  # fail loudly if the HIP library is missing
 
     rank, world, local = dist_setup(args.gpus)
@@ -189,8 +190,9 @@ def main():
     for b in range(pool):
         u = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
         d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
-        # global frame index of local frame j in batch b: b*n*world + rank + j*world (round robin)
-        X.synth_dev(u, d, n, 0, stride, seed, b * n * world + rank, world, 0, lo, hi)
+        # round-robin shard: local frame j of batch b is global frame first + j*step
+        first, gstep = shard.shard_range(b, n, rank, world)
+        X.synth_dev(u, d, n, 0, stride, seed, first, gstep, 0, lo, hi)
         umems.append(u)
         descss.append(d)
     torch.cuda.synchronize()
