@@ -25,6 +25,7 @@ import torch  # noqa: E402
 
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+KERNEL = "echo_kernel5<4>"  # the transform kernel xsk_gpu_echo_dev launches
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
@@ -120,16 +121,16 @@ def _cpu_model():
     return "unknown"
 
 
-def traffic_from_profiles(cfg):
-    """PMC-derived HBM bytes per launch, if a committed rocprofv3 --pmc summary exists."""
+def traffic_from_profiles(cfg, kernel):
+    """PMC-derived HBM bytes per launch from the committed rocprofv3 --pmc summary of this config
+    (tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled on gfx950),
+    or None when there is none for the kernel that ran."""
     p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
-    if os.path.exists(p):
-        try:
-            d = json.load(open(p))
-            return d.get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return None
+    return d.get("hbm_bytes_per_launch") if d.get("kernel") and d["kernel"] in kernel else None
 
 
 def host_inclusive(cfg, dev_index):
@@ -285,8 +286,8 @@ def main():
                        "rearm_in_timed_region": rearm_in_loop},
             "verified": bool(ok_all == world),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config),
-                         "kernel": "echo_kernel<4>", "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config, KERNEL),
+                         "kernel": KERNEL, "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": frame_bytes,
                          "read_ceiling_gbs": round(read_ceiling, 1)},
             "event_ms_per_step": round(ev_max / K, 4),

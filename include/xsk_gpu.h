@@ -18,9 +18,12 @@
  * Frame ownership contract (AF_XDP gives every frame its own >= 2048-byte UMEM chunk):
  *   - the UMEM base is 16-byte aligned and the UMEM size is a multiple of 16;
  *   - every frame exclusively owns the bytes [addr, addr + max(len, 64)) of the UMEM for the duration
- *     of a call (frames of one batch never overlap); the library only ever writes bytes
- *     [addr, addr + 38) of frames whose verdict is XSK_GPU_TX_REPLY, and only reads bytes inside
- *     [align16(addr), align16(addr) + 64) u [addr, addr + len).
+ *     of a call (frames of one batch never overlap); the library only changes bytes
+ *     [addr, addr + 38) of frames whose verdict is XSK_GPU_TX_REPLY (exactly the bytes the reference
+ *     rewrites), and only reads bytes inside [align16(addr), align16(addr) + 64) u [addr, addr + len);
+ *   - a 16-B aligned reply whose [addr, addr + 64) lies in the UMEM is stored as that whole 64-byte
+ *     window (bytes 38-63 are written back with the values they held), so HBM sees full sectors
+ *     instead of read-modify-write partial ones; unaligned replies are stored byte-exact.
  */
 #ifndef XSK_GPU_H
 #define XSK_GPU_H
@@ -103,7 +106,7 @@ struct xsk_gpu_rec {
 /* ------------------------------------------------------------------------------------------ */
 
 /* Bytes of device workspace xsk_gpu_echo_dev() needs for a batch of n frames on `device`
- * (per-workgroup counter partials; at most 64 KiB). */
+ * (per-workgroup counter partials; 32 B per 256 frames, at most 512 KiB). */
 size_t xsk_gpu_workspace_size(int device, uint32_t n);
 
 /* Transform n frames in place on the current HIP device.
