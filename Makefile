@@ -11,13 +11,16 @@ LIB      := xsknet_amd/libxsknet_amd.so
 
 all: $(LIB) oracle tools/echo_replay
 
-$(CSRC)/xsk_echo.o: $(CSRC)/xsk_echo.hip $(CSRC)/xsk_echo_kernels.h include/xsk_gpu.h
+DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
+HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_tune.o
+
+$(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(CSRC)/xsk_gpu_host.o: $(CSRC)/xsk_gpu_host.c include/xsk_gpu.h
 	$(CC) $(CFLAGS) -I$(ROCM)/include -c -o $@ $<
 
-$(LIB): $(CSRC)/xsk_echo.o $(CSRC)/xsk_gpu_host.o
+$(LIB): $(HIPOBJ) $(CSRC)/xsk_gpu_host.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libxsknet_amd.so
 
 tools/echo_replay: tools/echo_replay.c $(LIB) include/xsk_gpu.h

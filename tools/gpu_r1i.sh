@@ -9,7 +9,7 @@ run() { local name=$1 to=$2; shift 2
   echo "rc=$rc"; tail -3 "$O/$name.log"; return $rc; }
 run gputests 900 python -m pytest tests -m gpu -q -x --timeout 600 -p no:cacheprovider || exit 1
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
-run kb 600 python tools/kbench.py --reps 3 --pool 10 --layouts c2_s64,c3_s4096,c4_s2048 --variants 0,52 --grids -1 || exit 1
+run kb 600 python tools/kbench.py --reps 3 --pool 10 --layouts c2_s64,c3_s4096,c4_s2048 --variants 0,53 --grids -1 || exit 1
 grep variant $O/kb.log | python3 -c "
 import sys,json
 for l in sys.stdin:

@@ -6,7 +6,8 @@ Times each kernel launch with HIP events on the launch stream.  Two regimes:
   --pool K  : K distinct batches, launched back to back (each timed), re-armed after the sweep;
               with K batches >> Infinity Cache this is the bench's cold-data regime.
 Variants (xsk_gpu__echo_variant): 0/1/2/3 = ring depth P 4/8/2/6, 10+x = stream-only ceiling of the
-same P (LITE), 30+ = continuous-ring kernel, see xsk_echo.hip.  -1 = stream_read over the slab.
+same P (LITE), 50+ = the shipped row-streaming kernel at other settings, see xsk_tune.hip.
+-1 = stream_read over the slab.
 Prints one JSON line per (layout, variant, grid) to stdout.
 """
 import argparse

@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -20,19 +21,19 @@ KERNEL = "echo_kernel5"
 
 def per_launch(d, counter):
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-            if r["Counter_Name"] == counter and KERNEL in r["Kernel_Name"]]
-    return statistics.median(vals), len(vals)
+    rows = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter and KERNEL in r["Kernel_Name"]]
+    name = re.search(r"echo_kernel5<[^>]*>", rows[0]["Kernel_Name"]).group(0)
+    return statistics.median(float(r["Counter_Value"]) for r in rows), len(rows), name
 
 
 def main():
     fetch_dir, write_dir, algo, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    fk, nf = per_launch(fetch_dir, "FETCH_SIZE")
-    wk, nw = per_launch(write_dir, "WRITE_SIZE")
+    fk, nf, name = per_launch(fetch_dir, "FETCH_SIZE")
+    wk, nw, _ = per_launch(write_dir, "WRITE_SIZE")
     read_b = fk * 1024 * 2
     write_b = wk * 1024
     res = {
-        "kernel": KERNEL,
+        "kernel": name,
         "launches": {"fetch_pass": nf, "write_pass": nw},
         "fetch_size_kib_raw": fk, "write_size_kib_raw": wk,
         "read_bytes_per_launch": int(read_b), "write_bytes_per_launch": int(write_b),

@@ -12,6 +12,9 @@
 //   mode 6: mode 1 with default-policy (not nt) loads
 //   mode 7: mode 4 with nontemporal stores
 //   mode 8: + 64 B per frame into a contiguous side buffer (coalesced), not in place
+//   mode 9: header read only, 64 B per frame (4 lanes), no payload
+//   mode 10: + 64 B per frame of constant data stored right after the frame's loads are ISSUED
+//            (before they return): the write reaches the DRAM page the reads just opened
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,7 +35,19 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
             if (f >= n) break;
             uint8_t* fr = buf + (uint64_t)f * stride;
             u32x4 v[6];
-            if (MODE != 5) {
+            if (MODE == 10) {  // unconditional loads (stride >= 1536), then the store, then the waits
+#pragma unroll
+                for (int u = 0; u < 6; ++u) v[u] = __builtin_nontemporal_load((const u32x4*)(fr + 256u * u + 16u * k));
+                if (k < 4) {
+                    const u32x4 c = u32x4{f, 0x5A5A5A5Au, f, 0x01234567u};
+                    asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(fr + 16u * k), "v"(c) : "memory");
+                }
+#pragma unroll
+                for (int u = 0; u < 6; ++u) acc += (uint64_t)v[u].x + v[u].y + v[u].z + v[u].w;
+            } else if (MODE == 9) {
+                v[0] = k < 4 ? __builtin_nontemporal_load((const u32x4*)(fr + 16u * k)) : u32x4{0, 0, 0, 0};
+                acc += (uint64_t)v[0].x + v[0].y + v[0].z + v[0].w;
+            } else if (MODE != 5) {
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     const uint32_t ro = 256u * u + 16u * k;
@@ -98,6 +113,8 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 6: wexp_kernel<6><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 7: wexp_kernel<7><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 8: wexp_kernel<8><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
+        case 9: wexp_kernel<9><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
+        case 10: wexp_kernel<10><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

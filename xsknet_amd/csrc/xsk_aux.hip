@@ -1,0 +1,243 @@
+// xsk_aux.hip — bench / test utilities of the C ABI (not on the hot path): the synthetic frame
+// generator (bit-identical to oracle/echo_oracle.c), re-arm, the staged-mode header gather and the
+// read-only streaming ceiling.
+#include <errno.h>
+
+#include "../../include/xsk_gpu.h"
+#include "xsk_echo_kernels.h"
+#include "xsk_hip_util.h"
+
+using namespace xskgpu;
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// Synthetic frames: one wave per frame, bit-identical to oracle_synth_frame().
+// ------------------------------------------------------------------------------------------------
+struct SynthArgs {
+    uint8_t* umem;
+    uint64_t umem_size;
+    xsk_gpu_desc* descs;
+    uint32_t n;
+    uint64_t base_off, stride, seed, first, step;
+    int mode;
+    uint32_t len_lo, len_hi;
+};
+
+__device__ __constant__ uint32_t k_short_lens[13] = {0, 1, 13, 14, 19, 20, 21, 33, 34, 37, 38, 41, 42};
+
+__global__ __launch_bounds__(256) void synth_kernel(SynthArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t j = blockIdx.x * 4u + uniform(threadIdx.x >> 6);
+    if (j >= a.n) return;
+    const uint64_t gidx = a.first + (uint64_t)j * a.step;
+    const uint64_t K = mix64(a.seed ^ mix64(gidx));
+    const uint64_t r1 = mix64(K + 1), r2 = mix64(K + 2), r3 = mix64(K + 3), r4 = mix64(K + 4), r5 = mix64(K + 5);
+    uint32_t L = a.len_lo == a.len_hi ? a.len_lo : a.len_lo + (uint32_t)(r5 % (uint64_t)(a.len_hi - a.len_lo + 1));
+    const uint32_t s = a.mode == 1 ? (uint32_t)(r4 >> 32) % 20u : 0u;
+    if (s == 18) L = k_short_lens[(r5 >> 40) % 13];
+    const uint32_t W = ((L > 64 ? L : 64) + 15u) & ~15u;  // fill extent: whole 16-B blocks
+    const uint64_t addr = a.base_off + (uint64_t)j * a.stride;
+    uint8_t* frame = a.umem + addr;
+
+    // header dwords (little-endian), checksum fields zero for now
+    uint32_t hw[11];
+    const uint32_t eth = s == 6 ? 0x86DDu : s == 7 ? 0x8100u : 0x0800u;
+    const uint32_t vihl = s == 12 ? 0x46u : s == 13 ? 0x65u : 0x45u;
+    const uint32_t tl = (L >= 14 ? L - 14 : 0u) & 0xFFFFu;
+    const uint32_t frag = s == 14 ? 0x2000u : 0x4000u;
+    const uint32_t proto = s == 8 ? 6u : 1u;
+    const uint32_t itype = s == 9 ? 0u : s == 10 ? 13u : 8u;
+    const uint32_t icode = s == 11 ? 5u : 0u;
+    hw[0] = (uint32_t)r1;
+    hw[1] = ((uint32_t)(r1 >> 32) & 0xFFFFu) | ((uint32_t)r2 << 16);
+    hw[2] = (uint32_t)(r2 >> 16);
+    hw[3] = bswap16(eth) | (vihl << 16);
+    hw[4] = bswap16(tl) | ((uint32_t)(r2 >> 48) << 16);
+    hw[5] = bswap16(frag) | (64u << 16) | (proto << 24);
+    hw[6] = (uint32_t)r3 << 16;
+    hw[7] = (uint32_t)(r3 >> 16);
+    hw[8] = (uint32_t)(r3 >> 48) | (itype << 16) | (icode << 24);
+    hw[9] = ((uint32_t)r4 & 0xFFFFu) << 16;
+    hw[10] = ((uint32_t)r4 >> 16) & 0xFFFFu;
+    const bool garbage = s == 19;
+    const bool zero_icmp = s == 17;
+
+    // Build this lane's blocks (<= 4096/16/64 = 4 per lane) and the ICMP partial sum over [34, L).
+    const uint32_t nblk = (W + 15) / 16;
+    u32x4 blk[4];
+    uint32_t s_ic = 0;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const uint32_t b = lane + 64u * (uint32_t)it;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        if (b < nblk) {
+            const uint64_t p0 = mix64(K + 16 + 2 * (uint64_t)b), p1 = mix64(K + 16 + 2 * (uint64_t)b + 1);
+            uint32_t w[4] = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+            if (!garbage) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t k = 4 * b + (uint32_t)i;  // frame dword index
+                    if (k < 10) w[i] = hw[k];
+                    else if (k == 10) w[i] = (w[i] & 0xFFFF0000u) | hw[10];
+                    if (zero_icmp) {  // bytes [38, L) zero
+                        const int base = 4 * (int)k;
+                        const uint32_t z = keep_bytes(0xFFFFFFFFu, base, 38, (int)L);
+                        w[i] &= ~z;
+                    }
+                    s_ic += halves(keep_bytes(w[i], 4 * (int)k, 34, (int)L));
+                }
+            }
+            v = u32x4{w[0], w[1], w[2], w[3]};
+        }
+        blk[it] = v;
+    }
+    if (!garbage) {
+        const uint32_t tot = wave_sum_u32(s_ic);
+        uint32_t icc = (~bswap16(fold32(tot))) & 0xFFFFu;
+        if (s == 15) icc ^= 0x1234u;
+        uint32_t sip = (hw[3] >> 16) + halves(hw[4]) + halves(hw[5]) + halves(hw[6]) + halves(hw[7]) + (hw[8] & 0xFFFFu);
+        uint32_t ipc = (~bswap16(fold32(sip))) & 0xFFFFu;
+        if (s == 16) ipc ^= 0x5A5Au;
+        // bytes 24-25 live in block 1 (.z low half), bytes 36-37 in block 2 (.y low half); lanes 1, 2
+        if (lane == 1) blk[0].z = (blk[0].z & 0xFFFF0000u) | bswap16(ipc);
+        if (lane == 2) blk[0].y = (blk[0].y & 0xFFFF0000u) | bswap16(icc);
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const uint32_t b = lane + 64u * (uint32_t)it;
+        if (b < nblk) ((u32x4*)frame)[b] = blk[it];
+    }
+    if (lane == 0) {
+        xsk_gpu_desc dd;
+        dd.addr = addr;
+        dd.len = L;
+        dd.options = 0;
+        a.descs[j] = dd;
+    }
+}
+
+// Staged host mode: gather the 38 rewritten header bytes of every TX_REPLY frame into a packed
+// [n][48] array so the host can scatter them back into its UMEM (never touching unowned bytes).
+__global__ __launch_bounds__(256) void pack_headers_kernel(const uint8_t* umem, const xsk_gpu_desc* descs,
+                                                           const uint8_t* verdicts, uint32_t n, uint8_t* pack) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || verdicts[i] != XSK_GPU_TX_REPLY) return;
+    const uint8_t* p = umem + descs[i].addr;
+    uint8_t* q = pack + (uint64_t)i * 48u;
+    for (int k = 0; k < 38; ++k) q[k] = p[k];
+}
+
+// Re-arm TX_REPLY frames (lane per frame, byte granular: bench utility, not the hot path).
+__global__ __launch_bounds__(256) void rearm_kernel(uint8_t* umem, const xsk_gpu_desc* descs, const uint8_t* verdicts,
+                                                    uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n || verdicts[i] != XSK_GPU_TX_REPLY) return;
+    uint8_t* p = umem + descs[i].addr;
+    uint8_t t[6];
+    for (int k = 0; k < 6; ++k) t[k] = p[k];
+    for (int k = 0; k < 6; ++k) p[k] = p[6 + k];
+    for (int k = 0; k < 6; ++k) p[6 + k] = t[k];
+    for (int k = 0; k < 4; ++k) {
+        const uint8_t x = p[26 + k];
+        p[26 + k] = p[30 + k];
+        p[30 + k] = x;
+    }
+    p[34] = 8;
+    // csum_replace2(csum, 0, 8) on the LE-loaded field
+    uint32_t c = (uint32_t)p[36] | ((uint32_t)p[37] << 8);
+    uint32_t x = (~c) & 0xFFFFu;
+    x = (x + 0xFFFFu) & 0xFFFFu;
+    x += x < 0xFFFFu ? 1u : 0u;
+    x = (x + 8u) & 0xFFFFu;
+    x += x < 8u ? 1u : 0u;
+    x = (~x) & 0xFFFFu;
+    p[36] = (uint8_t)x;
+    p[37] = (uint8_t)(x >> 8);
+}
+
+// Read-only streaming ceiling: every byte loaded once with 16-B nontemporal loads.
+__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* src, uint64_t nvec, unsigned long long* out) {
+    uint64_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u;
+    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    for (; i + 3 * stride < nvec; i += 4 * stride) {
+        const u32x4 a0 = __builtin_nontemporal_load(src + i);
+        const u32x4 a1 = __builtin_nontemporal_load(src + i + stride);
+        const u32x4 a2 = __builtin_nontemporal_load(src + i + 2 * stride);
+        const u32x4 a3 = __builtin_nontemporal_load(src + i + 3 * stride);
+        acc += (uint64_t)a0.x + a0.y + a0.z + a0.w + a1.x + a1.y + a1.z + a1.w;
+        acc += (uint64_t)a2.x + a2.y + a2.z + a2.w + a3.x + a3.y + a3.z + a3.w;
+    }
+    for (; i < nvec; i += stride) {
+        const u32x4 a0 = __builtin_nontemporal_load(src + i);
+        acc += (uint64_t)a0.x + a0.y + a0.z + a0.w;
+    }
+    acc = wave_sum_u64(acc);
+    if ((threadIdx.x & 63u) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
+}  // namespace
+
+extern "C" {
+
+int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_descs, uint32_t n, uint64_t base_off,
+                      uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode, uint32_t len_lo,
+                      uint32_t len_hi, void* stream) {
+    if (n == 0) return 0;
+    if (!d_umem || !d_descs || (base_off & 15u) || (stride & 15u) || len_lo > len_hi || (mode != 0 && mode != 1) ||
+        ((uintptr_t)d_umem & 15u))
+        return -EINVAL;
+    const uint64_t w = ((len_hi > 64 ? len_hi : 64) + 15u) & ~15ull;
+    if (stride < w || w > 4096) return -EINVAL;
+    if (base_off + (uint64_t)(n - 1) * stride + w > umem_size) return -EINVAL;
+    SynthArgs a;
+    a.umem = (uint8_t*)d_umem;
+    a.umem_size = umem_size;
+    a.descs = d_descs;
+    a.n = n;
+    a.base_off = base_off;
+    a.stride = stride;
+    a.seed = seed;
+    a.first = first;
+    a.step = step;
+    a.mode = mode;
+    a.len_lo = len_lo;
+    a.len_hi = len_hi;
+    hipLaunchKernelGGL(synth_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int xsk_gpu_rearm_dev(void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts, uint32_t n,
+                      void* stream) {
+    if (n == 0) return 0;
+    if (!d_umem || !d_descs || !d_verdicts) return -EINVAL;
+    hipLaunchKernelGGL(rearm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (uint8_t*)d_umem, d_descs,
+                       d_verdicts, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
+                              uint32_t n, uint8_t* d_pack, void* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(pack_headers_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_umem, d_descs, d_verdicts, n, d_pack);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int xsk_gpu_stream_read_dev(const void* d_src, uint64_t bytes, uint64_t* d_out, void* stream) {
+    if (!d_src || !d_out || (bytes & 15u) || ((uintptr_t)d_src & 15u)) return -EINVAL;
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)cus * 8u), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)d_src, bytes / 16, (unsigned long long*)d_out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

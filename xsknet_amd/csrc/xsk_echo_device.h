@@ -1,0 +1,478 @@
+// xsk_echo_device.h — device code of the gfx950 (MI355X / CDNA4) ICMP-echo transform, shared by the
+// shipped entry point (xsk_echo.hip) and the tuning variants (xsk_tune.hip).
+//
+// Replaces, for a whole batch of AF_XDP descriptors at once, the per-frame call
+//   process_packet()   /root/reference/src/lib/xsk_receive.c:113-190   (gates, field swap, type 8->0,
+//   csum_replace2()    /root/reference/src/lib/xsk_receive.c:101-111    RFC 1624 incremental update)
+// and the counter updates of the batch loop at xsk_receive.c:171-172,229,233.  No MFMA: the op is
+// integer byte arithmetic and HBM bound.
+#pragma once
+
+#include "../../include/xsk_gpu.h"
+#include "xsk_echo_kernels.h"
+
+namespace xskgpu {
+namespace {
+
+constexpr int kTile = XSK_GPU_TILE_FRAMES;  // frames per wave tile
+constexpr int kWaves = 4;                   // waves per workgroup
+constexpr int kThreads = kTile * kWaves;    // 256
+constexpr int kWin = 64;                    // header window [a16, a16 + 64)
+constexpr int kShipU = 4;                   // shipped kernel: row-loads in flight per lane
+constexpr int kShipMinW = 6;                // shipped kernel: waves per SIMD it is register-bounded for
+constexpr uint32_t kMaxLen = 1u << 30;      // build-added descriptor sanity bound (XSK_GPU_MAX_LEN)
+
+struct EchoArgs {
+    uint8_t* umem;
+    uint64_t umem_size;
+    const xsk_gpu_desc* descs;
+    uint32_t n;
+    uint8_t* verdicts;
+    xsk_gpu_rec* recs;
+    unsigned long long* partials;  // [gridDim.x][4]: rx_packets, rx_bytes, tx_packets, tx_bytes
+};
+
+// Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
+constexpr int kRsrcFlags = 0x00020000;
+constexpr int kAuxNT = 2;  // nontemporal: payload bytes are read exactly once
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);  // keep it unsigned: no sign-extension
+}
+
+__device__ __forceinline__ uint32_t row_sum_dpp(uint32_t x) {  // lane 15 of each 16-lane row: row total
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    return x;
+}
+
+// Mask keeping the low nb bytes of a dword (nb <= 0: none, nb >= 4: all).
+__device__ __forceinline__ uint32_t dw_mask(int nb) {
+    return nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+}
+
+struct Counters {
+    uint64_t rxp = 0, rxb = 0, txp = 0, txb = 0;
+};
+
+// Counters: wave -> workgroup -> one partial row per workgroup (no atomics).
+__device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, unsigned long long (*s_cnt)[4],
+                                               uint32_t wave, uint32_t lane) {
+    if (!a.partials) return;
+    c.rxp = wave_sum_u64(c.rxp);
+    c.rxb = wave_sum_u64(c.rxb);
+    c.txp = wave_sum_u64(c.txp);
+    c.txb = wave_sum_u64(c.txb);
+    if (lane == 0) {
+        s_cnt[wave][0] = c.rxp;
+        s_cnt[wave][1] = c.rxb;
+        s_cnt[wave][2] = c.txp;
+        s_cnt[wave][3] = c.txb;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long s = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) s += s_cnt[w][threadIdx.x];
+        a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {  // uniform result (SGPRs)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    return ((uint64_t)uniform((uint32_t)(x >> 32)) << 32) | (uint64_t)uniform((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o, 64);
+        x = y > x ? y : x;
+    }
+    return ((uint64_t)uniform((uint32_t)(x >> 32)) << 32) | (uint64_t)uniform((uint32_t)x);
+}
+
+// Stream loaders: `in` = the block lies (at least partly) inside the lane's frame.
+struct WinLoader {  // tile-wide buffer window; out-of-range offsets return zeros, no memory access
+    static constexpr bool kZeroFill = true;
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t rel;  // frame's a16 relative to the window base
+    __device__ __forceinline__ u32x4 load(uint32_t ro, bool in) const {
+        return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(in ? rel + ro : 0x80000000u), 0, kAuxNT);
+    }
+};
+struct FarLoader {  // 64-bit addresses; lanes past the frame re-read its first block, then select zeros
+    static constexpr bool kZeroFill = true;
+    const uint8_t* fbase;
+    __device__ __forceinline__ u32x4 load(uint32_t ro, bool in) const {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)(fbase + (in ? ro : 0u)));
+        return in ? v : u32x4{0u, 0u, 0u, 0u};
+    }
+};
+
+// ================================================================================================
+// The transform kernel (shipped).  One read of every byte.  The payload is streamed by 16-lane DPP rows (row q of step s
+// owns frame 4s+q, 256-B row-loads), but the stream starts at row byte 0: the first four lanes of a
+// frame's first row-load carry its 64-B header window, which they drop into the frame's LDS row, so
+// no separate header read is issued.  Each frame's loads span max(frame end, window end) row bytes;
+// the payload sum takes row bytes [64, rowhi) and the header phase the window part.  Patched windows
+// of 16-B aligned replies leave as whole 64-B sectors, 16 frames per wave-store, after the tile.
+// ================================================================================================
+// One frame's row sums, both in the absolute-alignment domain (64-bit sums of LE dwords):
+//   ic: ICMP bytes, row [off + 34, rowhi)      ip: IPv4 header bytes, row [off + 14, ip_hi)
+struct RowSums {
+    uint64_t ic = 0, ip = 0;
+};
+
+__device__ __forceinline__ uint64_t sum_dw(u32x4 x) {
+    return (uint64_t)x.x + (uint64_t)x.y + (uint64_t)x.z + (uint64_t)x.w;
+}
+// sum of the bytes of block x (row bytes [ro, ro+16)) that lie in [lo, hi)
+__device__ __forceinline__ uint64_t sum_range(u32x4 x, int ro, int lo, int hi) {
+    return (uint64_t)keep_bytes(x.x, ro, lo, hi) + (uint64_t)keep_bytes(x.y, ro + 4, lo, hi) +
+           (uint64_t)keep_bytes(x.z, ro + 8, lo, hi) + (uint64_t)keep_bytes(x.w, ro + 12, lo, hi);
+}
+
+// Per-frame metadata of a tile, kept in LDS so that the row streams of step s read frame 4s+q's
+// entry by broadcast LDS reads instead of holding it in VGPRs across the stream loop.
+struct FrameMeta {
+    uint32_t rel;     // a16 relative to the tile's buffer window (fast path)
+    uint32_t rowhi;   // frame end, row coordinates (0 unless parsed)
+    uint32_t lim;     // row bytes to load: max(rowhi, window bytes in the UMEM)
+    uint32_t packed;  // off | iphi << 8 | flags << 16 (1 ok, 2 parse)
+    uint32_t nit;     // 256-B row-loads: ceil(lim / 256)
+    uint32_t addr_lo, addr_hi, len;
+};
+
+// One frame's row stream: row-loads j = 0 .. ns-1 (lane k takes row bytes [256 j + 16 k, +16)).  The
+// first row-load carries the 64-B window: lanes 0-3 drop it into the frame's LDS row and every lane
+// sums its bytes by exact range (ICMP [off+34, rowhi), IPv4 header [off+14, iphi)); later blocks only
+// need the frame-end mask.
+template <int U, class L>
+__device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t f_rowhi, uint32_t f_lim,
+                                             uint32_t f_off, uint32_t f_iphi, uint32_t k, uint8_t* hdr_row,
+                                             RowSums& rs) {
+    if (ns == 1u) {
+        const uint32_t ro = 16u * k;
+        const u32x4 x = ld.load(ro, ro < f_lim);
+        if (k < 4u) *(u32x4*)(hdr_row + ro) = x;
+        rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
+        rs.ic += sum_range(x, (int)ro, (int)f_off + 34, (int)f_rowhi);
+        return;
+    }
+    for (uint32_t j0 = 0; j0 < ns; j0 += U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
+            v[u] = ld.load(ro, ro < f_lim);  // past the frame: zeros, no memory access
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
+            const u32x4 x = v[u];
+            if (u == 0 && j0 == 0u) {
+                if (k < 4u) *(u32x4*)(hdr_row + ro) = x;
+                rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
+                rs.ic += sum_range(x, (int)ro, (int)f_off + 34, (int)f_rowhi);
+            } else {
+                const int nb = (int)(f_rowhi - min(ro, f_rowhi));      // frame bytes in this block
+                if (__ballot(nb > 0 && nb < 16) != 0ull) {             // a block that ends a frame
+                    u32x4 y = x;
+                    y.x &= dw_mask(nb);
+                    y.y &= dw_mask(nb - 4);
+                    y.z &= dw_mask(nb - 8);
+                    y.w &= dw_mask(nb - 12);
+                    rs.ic += sum_dw(y);
+                } else {
+                    rs.ic += sum_dw(x);  // whole block in the frame, or zeros past it
+                }
+            }
+        }
+    }
+}
+
+// Header work of one frame (lane = frame) from its LDS row and its two folded row sums.
+__device__ __forceinline__ bool header_phase5(const EchoArgs& a, uint8_t* row, uint32_t ip_raw, uint32_t ic_raw,
+                                              uint64_t addr, uint32_t len, bool live, bool ok, bool parse,
+                                              uint32_t fi, Counters& cnt) {
+    const uint32_t off = (uint32_t)addr & 15u;
+    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+    uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+
+    // parsed fields (xsk_receive.c:135,140,144,157)
+    const uint32_t eth_proto = parse ? (((h[3] & 0xFFu) << 8) | ((h[3] >> 8) & 0xFFu)) : 0u;
+    const uint32_t vihl = parse ? (h[3] >> 16) & 0xFFu : 0u;
+    const uint32_t proto = parse ? h[5] >> 24 : 0u;
+    const uint32_t itype = parse ? (h[8] >> 16) & 0xFFu : 0u;
+    const uint32_t icode = parse ? h[8] >> 24 : 0u;
+    const uint32_t csum_le = parse ? h[9] & 0xFFFFu : 0u;  // the reference's uint16_t load (:157)
+
+    uint32_t verdict;
+    if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+    else if (len < 20) verdict = XSK_GPU_DROP_SHORT;                 // :123-133
+    else if (eth_proto != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;  // :135
+    else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;           // :140
+    else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;           // :144
+    else verdict = XSK_GPU_TX_REPLY;
+    const bool tx = verdict == XSK_GPU_TX_REPLY;
+
+    // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY), xsk_receive.c:101-111,157
+    uint32_t c16 = (~csum_le) & 0xFFFFu;
+    c16 = (c16 + 0xFFF7u) & 0xFFFFu;  // csum += ~old  (old = 8)
+    c16 += c16 < 0xFFF7u ? 1u : 0u;   // end-around carry; csum += new (0) is a no-op
+    const uint32_t csum_new_le = tx ? (~c16) & 0xFFFFu : csum_le;
+
+    // RFC 1071 sums of the input frame (build-added verification fields)
+    uint32_t ip_sum = fold32(ip_raw);
+    uint32_t ic_sum = fold32(ic_raw);
+    if (!((uint32_t)addr & 1u)) {
+        ip_sum = bswap16(ip_sum);
+        ic_sum = bswap16(ic_sum);
+    }
+    uint32_t flags = 0;
+    if (parse && len >= 34 && ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
+    if (parse && len >= 42 && ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
+
+    // echo-reply rewrite, xsk_receive.c:148-157 (bytes 0-11, 26-34, 36-37)
+    bool wb = false;
+    if (tx) {
+        const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
+        const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
+        const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
+        const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
+        const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
+        const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
+        if (off == 0 && a.umem_size - addr >= (uint64_t)kWin) {
+            uint32_t* r32 = (uint32_t*)row;  // patched in LDS, stored as a whole window by the caller
+            r32[0] = n0;
+            r32[1] = n1;
+            r32[2] = n2;
+            r32[6] = n6;
+            r32[7] = n7;
+            r32[8] = n8;
+            r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+            wb = true;
+        } else {
+            uint8_t* pkt = a.umem + addr;
+            if ((off & 3u) == 0) {
+                uint32_t* p32 = (uint32_t*)pkt;
+                p32[0] = n0;
+                p32[1] = n1;
+                p32[2] = n2;
+                p32[6] = n6;
+                p32[7] = n7;
+                p32[8] = n8;
+                *(uint16_t*)(pkt + 36) = (uint16_t)csum_new_le;
+            } else {
+                const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
+#pragma unroll
+                for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+                for (int b = 0; b < 12; ++b) pkt[24 + b] = (uint8_t)(w[3 + (b >> 2)] >> (8 * (b & 3)));
+                pkt[36] = (uint8_t)csum_new_le;
+                pkt[37] = (uint8_t)(csum_new_le >> 8);
+            }
+        }
+    }
+    if (live) {
+        if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
+        if (a.recs) {
+            u32x4 r;
+            r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+            r.y = icode | (vihl << 8) | (eth_proto << 16);
+            r.z = (parse ? bswap16(csum_le) : 0u) | ((parse ? bswap16(csum_new_le) : 0u) << 16);
+            r.w = (parse ? ip_sum : 0u) | ((parse ? ic_sum : 0u) << 16);
+            ((u32x4*)a.recs)[fi] = r;
+        }
+        cnt.rxp += 1;
+        cnt.rxb += len;
+        if (tx) {
+            cnt.txp += 1;
+            cnt.txb += len;
+        }
+    }
+    return wb;
+}
+
+template <int U, int MINW>
+__global__ __launch_bounds__(kThreads, MINW) void echo_kernel5(EchoArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kWin];
+    __shared__ __attribute__((aligned(16))) FrameMeta s_meta[kWaves][kTile];
+    __shared__ uint32_t s_sum[kWaves][2][kTile];  // [ic, ip] folded row sums per frame
+    __shared__ unsigned long long s_cnt[kWaves][4];
+
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    uint8_t* rows = s_hdr[wave];
+    FrameMeta* meta = s_meta[wave];
+    uint32_t* sums_ic = s_sum[wave][0];
+    uint32_t* sums_ip = s_sum[wave][1];
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t nwaves = gridDim.x * kWaves;
+    Counters cnt;
+    uint32_t lane = threadIdx.x & 63u;
+
+    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += nwaves) {
+        // A wave normally runs one tile: keep the compiler from hoisting lane-derived values out of
+        // this loop into VGPRs that would stay live (and cut occupancy) for the whole kernel.
+        asm volatile("" : "+v"(lane));
+        const uint32_t q = lane >> 4, k = lane & 15u;
+        // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i -> LDS metadata ----------
+        uint32_t nit;
+        uint64_t wlo, span;
+        bool short_tile;  // every frame of the tile lies within its 64-B window
+        {
+            const uint32_t fi = t * kTile + lane;
+            u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
+            if (fi < a.n) dsc = *(const u32x4*)(a.descs + fi);
+            const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
+            const uint32_t len = dsc.z;
+            // build-added bounds check; the reference reads bytes [0,38) whenever len >= 20
+            const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+            const bool ok = fi < a.n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+            const bool parse = ok && len >= 20;
+            const uint64_t a16 = addr & ~15ull;
+            const uint32_t off = (uint32_t)addr & 15u;
+            const uint32_t rowhi = parse ? off + len : 0u;
+            const uint32_t win = parse ? (uint32_t)min(a.umem_size - a16, (uint64_t)kWin) : 0u;
+            const uint32_t lim = max(rowhi, win);
+            nit = (lim + 255u) >> 8;
+            short_tile = __ballot(lim > (uint32_t)kWin) == 0ull;
+            if (short_tile) {  // short tiles use per-frame 64-bit loads: no window needed
+                wlo = 0;
+                span = ~0ull;
+            } else {
+                wlo = wave_min_u64(nit ? a16 : ~0ull);
+                span = wave_max_u64(nit ? a16 + lim : 0ull) - wlo;
+            }
+            FrameMeta m;
+            m.rel = nit && !short_tile ? (uint32_t)(a16 - wlo) : 0u;
+            m.rowhi = rowhi;
+            m.lim = lim;
+            m.packed = off | ((parse ? off + min(len, 34u) : 0u) << 8) | ((ok ? 1u : 0u) << 16) |
+                       ((parse ? 2u : 0u) << 16);
+            m.nit = nit;
+            m.addr_lo = dsc.x;
+            m.addr_hi = dsc.y;
+            m.len = len;
+            meta[lane] = m;
+        }
+
+        // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS ---------------------
+        if (__ballot(nit != 0u) != 0ull) {
+            __builtin_amdgcn_wave_barrier();
+            const bool fast = span < 0x80000000ull;  // wave-uniform
+            WinLoader ld;
+            ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
+                                                     fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
+            if (short_tile) {
+                // ---- short tile (every frame within its 64-B window): 4 lanes per frame, 16 frames per
+                // wave-load (all four issued before the first is used), quad DPP reduction
+                const uint32_t kk = lane & 3u, ro = 16u * kk;
+                u32x4 x[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const FrameMeta& fm = meta[(uint32_t)r * 16u + (lane >> 2)];
+                    const uint64_t fa = (((uint64_t)fm.addr_hi) << 32) | (uint64_t)fm.addr_lo;
+                    const bool in = ro < fm.lim;
+                    x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? (fa & ~15ull) + ro : 0ull)));
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                    const FrameMeta& fm = meta[f];
+                    const uint32_t f_packed = fm.packed;
+                    const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                    *(u32x4*)(rows + f * kWin + ro) = v;
+                    const int f_off = (int)(f_packed & 0xFFu), f_iphi = (int)((f_packed >> 8) & 0xFFu);
+                    uint32_t rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
+                    uint32_t ric = fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
+                    rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);  // quad [1,0,3,2]
+                    ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);
+                    rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0x4E, 0xF, 0xF, false);  // quad [2,3,0,1]
+                    ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);
+                    if (kk == 0u) {
+                        sums_ic[f] = ric;
+                        sums_ip[f] = rip;
+                    }
+                }
+            } else
+            for (uint32_t s = 0; s < 16; ++s) {
+                const uint32_t f = 4u * s + q;
+                const FrameMeta& fm = meta[f];  // broadcast read: one entry per 16-lane row
+                const uint32_t f_nit = fm.nit;
+                const uint32_t ns = max(max(rdlane(f_nit, 0), rdlane(f_nit, 16)), max(rdlane(f_nit, 32), rdlane(f_nit, 48)));
+                if (ns == 0) continue;
+                const uint32_t f_rowhi = fm.rowhi, f_lim = fm.lim, f_packed = fm.packed;
+                const uint32_t f_off = f_packed & 0xFFu, f_iphi = (f_packed >> 8) & 0xFFu;
+                RowSums rs;
+                if (fast) {
+                    ld.rel = fm.rel;
+                    stream_frame<U>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kWin, rs);
+                } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
+                    FarLoader fl;
+                    fl.fbase = a.umem + (f_nit ? ((((uint64_t)fm.addr_hi) << 32) | (uint64_t)fm.addr_lo) & ~15ull : 0ull);
+                    stream_frame<U>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kWin, rs);
+                }
+                const uint32_t ric = row_sum_dpp(fold64(rs.ic));
+                const uint32_t rip = row_sum_dpp(fold64(rs.ip));
+                if (k == 15u) {
+                    sums_ic[f] = ric;
+                    sums_ip[f] = rip;
+                }
+            }
+        }
+
+        // ---- 3. header phase (lane = frame) ----------------------------------------------------------
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const FrameMeta m = meta[lane];
+        const uint32_t fi = t * kTile + lane;
+        const uint64_t addr = (uint64_t)m.addr_lo | ((uint64_t)m.addr_hi << 32);
+        const bool ok = (m.packed >> 16) & 1u, parse = (m.packed >> 17) & 1u;
+        const uint32_t ic_raw = m.nit ? sums_ic[lane] : 0u;
+        const uint32_t ip_raw = m.nit ? sums_ip[lane] : 0u;
+        const bool wb = header_phase5(a, rows + lane * kWin, ip_raw, ic_raw, addr, m.len, fi < a.n, ok, parse, fi, cnt);
+
+        // ---- 4. patched windows -> UMEM: 16 frames x 64 B per wave-store, whole 64-B sectors ---------
+        const uint64_t wbm = __ballot(wb);
+        if (wbm) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                const uint32_t kk = lane & 3u;
+                if ((wbm >> f) & 1ull) {
+                    const uint64_t fa = (uint64_t)meta[f].addr_lo | ((uint64_t)meta[f].addr_hi << 32);
+                    const u32x4 w = *(const u32x4*)(rows + f * kWin + 16u * kk);
+                    *(u32x4*)(a.umem + fa + 16u * kk) = w;
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next tile
+    }
+    store_partials(a, cnt, s_cnt, wave, lane);
+}
+
+// Launch geometry: one workgroup per kWaves tiles (the dispatcher balances ragged tiles better than
+// a persistent grid: 315 vs 347 us at c3), capped so the partials workspace stays <= 512 KiB (the
+// kernel's tile loop covers larger batches).
+constexpr uint32_t kMaxGrid = 16384;
+inline uint32_t echo_grid(uint32_t n) {
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    uint32_t g = (ntiles + kWaves - 1) / kWaves;
+    if (g > kMaxGrid) g = kMaxGrid;
+    return g < 1 ? 1 : g;
+}
+
+}  // namespace
+}  // namespace xskgpu

@@ -1,0 +1,372 @@
+// xsk_tune.hip — kernel variants for the tuning sweep (tools/kbench.py) and the parity test of every
+// variant (tests/test_gpu_parity.py::test_kernel_variants_parity).  Not on the product path.
+//
+//   0-6   v2 "wave per frame": one wave streams each frame of its 64-frame tile in 1 KiB wave-loads,
+//         P loads in flight through a ring over the tile's chunk list, header windows by LDS-DMA,
+//         one whole-wave DPP reduction per frame, 38-B partial header stores (the first design;
+//         DESIGN.md §3 has the measurements that replaced it)
+//   10-13 v2 LITE: stream and sum every frame byte, nothing else (a layout read ceiling)
+//   21-27 v2 ablations (ABL bits: 1 no header store, 2 no records/verdicts, 4 no header DMA)
+//   50-54 the shipped row-streaming kernel at other U (loads in flight) / occupancy settings
+#include <errno.h>
+
+#include "xsk_echo_device.h"
+#include "xsk_hip_util.h"
+
+using namespace xskgpu;
+
+namespace {
+
+// One slot of the streaming ring.
+struct Slot {
+    u32x4 v;         // 16 payload bytes of this lane
+    uint32_t nv;     // valid bytes of v (0..16)
+    uint32_t frame;  // owning frame (lane index in the tile), wave-uniform
+    uint32_t last;   // 1 if this chunk closes its frame, wave-uniform
+};
+
+// Wave-wide u32 sum with DPP row shifts + row broadcasts (no LDS traffic): after the four row_shr
+// steps lane 15 of each 16-lane row holds the row's inclusive sum; row_bcast:15 and row_bcast:31
+// carry rows 0..2 into lane 63.  Returns the total (wave-uniform, SGPR).
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return rdlane(x, 63);
+}
+
+// Issue the 16-B load of this lane for chunk g of the tile's flattened chunk list.  Branch-free on
+// the vector side: a raw buffer load whose descriptor (wave-uniform, SGPRs) spans exactly the bytes of
+// the chunk that lie inside the frame, so lanes past the frame end read zeros without touching memory,
+// and nothing forces a wait before the data is consumed P chunks later.
+template <int WIN>
+__device__ __forceinline__ void issue_chunk(Slot& s, uint32_t g, uint32_t T, uint32_t end, uint32_t nch,
+                                            uint32_t a16_lo, uint32_t a16_hi, uint32_t rowhi, const uint8_t* umem,
+                                            uint32_t lane) {
+    uint32_t f = 0, nrec = 0, last = 0, c = 0, f_rowhi = 0;
+    uint64_t base = 0;
+    if (g < T) {  // wave-uniform
+        // chunk g belongs to the first frame whose inclusive chunk-prefix end exceeds g
+        f = (uint32_t)__popcll(__ballot(end <= g));
+        const uint32_t f_end = rdlane(end, f);
+        const uint32_t f_nch = rdlane(nch, f);
+        c = g - (f_end - f_nch);
+        base = ((uint64_t)rdlane(a16_hi, f) << 32) | (uint64_t)rdlane(a16_lo, f);
+        f_rowhi = rdlane(rowhi, f);
+        const uint32_t cstart = (uint32_t)WIN + c * 1024u;  // row coordinates
+        const uint32_t rem = f_rowhi - cstart;             // > 0 by construction
+        nrec = rem >= 1024u ? 1024u : ((rem + 15u) & ~15u);
+        last = (c + 1 == f_nch) ? 1u : 0u;
+        base += cstart;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(umem + base), (short)0, (int)nrec, kRsrcFlags);
+    s.v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(lane * 16u), 0, kAuxNT);
+    const int32_t rem = (int32_t)(f_rowhi - ((uint32_t)WIN + c * 1024u + lane * 16u));
+    s.nv = g < T ? (rem <= 0 ? 0u : (rem >= 16 ? 16u : (uint32_t)rem)) : 0u;
+    s.frame = f;
+    s.last = last;
+}
+
+// P    : 1 KiB wave-loads kept in flight per wave (ring depth)
+// LITE : ablation / layout ceiling — stream every frame byte from offset 0 and sum it, nothing else
+// ABL (ablation bits, tuning sweep only; 0 in every shipped launch): 1 = skip header write-back,
+// 2 = skip records/verdicts, 4 = skip header DMA (header from stale LDS)
+template <int P, bool LITE, int MINW = 1, int ABL = 0>
+__global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
+    constexpr int WIN = LITE ? 0 : kWin;
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves][kTile * kWin];
+    __shared__ unsigned long long s_cnt[kWaves][4];
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    uint8_t* rows = s_hdr[wave];
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t nwaves = gridDim.x * kWaves;
+
+    uint64_t c_rxp = 0, c_rxb = 0, c_txp = 0, c_txb = 0;
+
+    uint32_t t = blockIdx.x * kWaves + wave;
+    // descriptor of this lane's frame in the first tile (next tiles are prefetched one tile ahead)
+    u32x4 dsc = *(const u32x4*)(a.descs + min(t * kTile + lane, a.n - 1));
+    for (; t < ntiles; t += nwaves) {
+        // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ------------------------
+        const uint32_t fi = t * kTile + lane;
+        const bool live = fi < a.n;
+        const uint64_t addr = live ? ((uint64_t)dsc.x | ((uint64_t)dsc.y << 32)) : 0;
+        const uint32_t len = live ? dsc.z : 0u;
+        {
+            const uint32_t tn = t + nwaves;  // prefetch the next tile's descriptors
+            dsc = *(const u32x4*)(a.descs + min(tn * kTile + lane, a.n - 1));
+        }
+        // build-added bounds check; the reference reads bytes [0,38) whenever len >= 20
+        const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+        const bool ok = live && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+        const bool parse = ok && (LITE || len >= 20);
+        const uint32_t a16_lo = (uint32_t)addr & ~15u;
+        const uint32_t a16_hi = (uint32_t)(addr >> 32);
+        const uint32_t off = (uint32_t)addr & 15u;
+        // frame end in row coordinates (row 0 = a16); < 2^31 because len <= kMaxLen
+        const uint32_t rowhi = parse ? off + len : 0u;
+
+        // ---- 2. streaming chunk list of the tile: bytes [WIN, rowhi) of each frame, 1 KiB chunks ----
+        const uint32_t nch = rowhi > (uint32_t)WIN ? (rowhi - (uint32_t)WIN + 1023u) >> 10 : 0u;
+        uint32_t end = nch;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)end, o, 64);
+            if (lane >= (uint32_t)o) end += y;
+        }
+        const uint32_t T = rdlane(end, 63);
+        Slot ring[P];
+#pragma unroll
+        for (int u = 0; u < P; ++u)
+            issue_chunk<WIN>(ring[u], (uint32_t)u, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
+
+        // ---- 3. header windows -> LDS by DMA (global_load_lds): 16 frames x 64 B per instruction ----
+        if (!LITE && !(ABL & 4)) {
+            const uint32_t row_need = parse ? min(off + (uint32_t)need, (uint32_t)kWin) : 0u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = r * 16 + (int)(lane >> 2);
+                const uint32_t k = lane & 3u;
+                const uint32_t f_lo = (uint32_t)__shfl((int)a16_lo, f, 64);
+                const uint32_t f_hi = (uint32_t)__shfl((int)a16_hi, f, 64);
+                const uint32_t f_need = (uint32_t)__shfl((int)row_need, f, 64);
+                // unneeded blocks read the (always mapped) UMEM base; those LDS bytes are never used
+                const uint64_t src = 16u * k < f_need ? ((((uint64_t)f_hi) << 32) | (uint64_t)f_lo) + 16u * k : 0ull;
+                __builtin_amdgcn_global_load_lds((const void*)(a.umem + src),
+                                                 (__attribute__((address_space(3))) void*)(rows + r * 1024), 16, 0, 0);
+            }
+        }
+
+        // ---- 4. drain the stream: per-lane 64-bit sums, one DPP wave reduction per frame ------------
+        uint64_t acc = 0;
+        uint32_t sres = 0;  // this lane's frame: stream part of the ICMP sum (absolute domain)
+        for (uint32_t g0 = 0; g0 < T; g0 += P) {
+#pragma unroll
+            for (int u = 0; u < P; ++u) {
+                const uint32_t g = g0 + (uint32_t)u;
+                if (g < T) {
+                    u32x4 v = ring[u].v;
+                    const uint32_t nv = ring[u].nv;
+                    if (nv < 16u) {
+                        v.x = keep_bytes(v.x, 0, 0, (int)nv);
+                        v.y = keep_bytes(v.y, 4, 0, (int)nv);
+                        v.z = keep_bytes(v.z, 8, 0, (int)nv);
+                        v.w = keep_bytes(v.w, 12, 0, (int)nv);
+                    }
+                    acc += (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+                    if (ring[u].last) {
+                        const uint32_t tot = wave_sum_dpp(fold64(acc));
+                        sres = lane == ring[u].frame ? tot : sres;  // hand the sum to the owning lane
+                        acc = 0;
+                    }
+                }
+                issue_chunk<WIN>(ring[u], g + (uint32_t)P, T, end, nch, a16_lo, a16_hi, rowhi, a.umem, lane);
+            }
+        }
+
+        if (LITE) {
+            if (live) {
+                c_rxp += 1;
+                c_rxb += len;
+                c_txb += sres;  // keeps the stream live
+            }
+            continue;
+        }
+
+        // ---- 5. header fields from LDS (the DMA is older than every stream load: already landed) ----
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint8_t* row = rows + lane * kWin;
+        const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+        const uint32_t sh = off & 3u;
+        uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
+#pragma unroll
+        for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], sh);
+        uint32_t d[16];  // absolute (16-B aligned) dwords of the window
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32x4 x = ((const u32x4*)row)[q];
+            d[4 * q + 0] = x.x;
+            d[4 * q + 1] = x.y;
+            d[4 * q + 2] = x.z;
+            d[4 * q + 3] = x.w;
+        }
+        // one's-complement partials in the absolute-alignment domain (RFC 1071 byte-order rule)
+        const int ip_lo = (int)off + 14;
+        const int ip_hi = parse ? (int)off + (int)min(len, 34u) : ip_lo;
+        const int ic_lo = (int)off + 34;
+        const int ic_hi = parse ? (int)min(rowhi, (uint32_t)kWin) : 0;
+        uint32_t s_ip = 0, s_ic = 0;
+#pragma unroll
+        for (int j = 3; j < 13; ++j) s_ip += halves(keep_bytes(d[j], 4 * j, ip_lo, ip_hi));
+#pragma unroll
+        for (int j = 8; j < 16; ++j) s_ic += halves(keep_bytes(d[j], 4 * j, ic_lo, ic_hi));
+
+        // parsed fields (xsk_receive.c:135,140,144,157)
+        const uint32_t eth_proto = parse ? (((h[3] & 0xFFu) << 8) | ((h[3] >> 8) & 0xFFu)) : 0u;
+        const uint32_t vihl = parse ? (h[3] >> 16) & 0xFFu : 0u;
+        const uint32_t proto = parse ? h[5] >> 24 : 0u;
+        const uint32_t itype = parse ? (h[8] >> 16) & 0xFFu : 0u;
+        const uint32_t icode = parse ? h[8] >> 24 : 0u;
+        const uint32_t csum_le = parse ? h[9] & 0xFFFFu : 0u;  // the reference's uint16_t load (:157)
+
+        uint32_t verdict;
+        if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+        else if (len < 20) verdict = XSK_GPU_DROP_SHORT;                 // :123-133
+        else if (eth_proto != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;  // :135
+        else if (proto != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;           // :140
+        else if (itype != 8u) verdict = XSK_GPU_DROP_NOT_ECHO;           // :144
+        else verdict = XSK_GPU_TX_REPLY;
+        const bool tx = verdict == XSK_GPU_TX_REPLY;
+
+        // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY), xsk_receive.c:101-111,157
+        uint32_t c16 = (~csum_le) & 0xFFFFu;
+        c16 = (c16 + 0xFFF7u) & 0xFFFFu;  // csum += ~old  (old = 8)
+        c16 += c16 < 0xFFF7u ? 1u : 0u;   // end-around carry
+        // csum += new (new = 0) and its carry test are no-ops
+        const uint32_t csum_new_le = tx ? (~c16) & 0xFFFFu : csum_le;
+
+        // ---- 6. checksums of the input frame (build-added verification fields) --------------------
+        const uint32_t odd = (uint32_t)addr & 1u;
+        uint32_t ip_sum = fold32(s_ip);
+        uint32_t ic_sum = fold32(s_ic + sres);
+        if (!odd) {
+            ip_sum = bswap16(ip_sum);
+            ic_sum = bswap16(ic_sum);
+        }
+        uint32_t flags = 0;
+        if (parse && len >= 34 && ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
+        if (parse && len >= 42 && ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
+
+        // ---- 7. echo-reply rewrite, xsk_receive.c:148-157 (bytes 0-11, 26-34, 36-37) -------------
+        if (tx && !(ABL & 1)) {
+            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
+            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
+            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
+            const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
+            const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
+            const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
+            uint8_t* pkt = a.umem + addr;
+            if ((addr & 3u) == 0) {
+                uint32_t* p32 = (uint32_t*)pkt;
+                p32[0] = n0;
+                p32[1] = n1;
+                p32[2] = n2;
+                p32[6] = n6;
+                p32[7] = n7;
+                p32[8] = n8;
+                *(uint16_t*)(pkt + 36) = (uint16_t)csum_new_le;
+            } else {
+                const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
+#pragma unroll
+                for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+#pragma unroll
+                for (int b = 0; b < 12; ++b) pkt[24 + b] = (uint8_t)(w[3 + (b >> 2)] >> (8 * (b & 3)));
+                pkt[36] = (uint8_t)csum_new_le;
+                pkt[37] = (uint8_t)(csum_new_le >> 8);
+            }
+        }
+
+        // ---- 8. verdicts, records, counters --------------------------------------------------------
+        if (live) {
+            if (a.verdicts && !(ABL & 2)) a.verdicts[fi] = (uint8_t)verdict;
+            if (a.recs && !(ABL & 2)) {
+                u32x4 r;
+                r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+                r.y = icode | (vihl << 8) | (eth_proto << 16);
+                r.z = (parse ? bswap16(csum_le) : 0u) | ((parse ? bswap16(csum_new_le) : 0u) << 16);
+                r.w = (parse ? ip_sum : 0u) | ((parse ? ic_sum : 0u) << 16);
+                ((u32x4*)a.recs)[fi] = r;
+            }
+            c_rxp += 1;
+            c_rxb += len;
+            if (tx) {
+                c_txp += 1;
+                c_txb += len;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next tile's DMA
+    }
+
+    // ---- counters: wave -> workgroup -> one partial row per workgroup (no atomics) -----------------
+    if (a.partials) {
+        c_rxp = wave_sum_u64(c_rxp);
+        c_rxb = wave_sum_u64(c_rxb);
+        c_txp = wave_sum_u64(c_txp);
+        c_txb = wave_sum_u64(c_txb);
+        if (lane == 0) {
+            s_cnt[wave][0] = c_rxp;
+            s_cnt[wave][1] = c_rxb;
+            s_cnt[wave][2] = c_txp;
+            s_cnt[wave][3] = c_txb;
+        }
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            unsigned long long s = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) s += s_cnt[w][threadIdx.x];
+            a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Internal (not in include/xsk_gpu.h): kernel variants for the tuning sweep in tools/kbench.py.
+//   variant: 0 <P=4>, 1 <P=8>, 2 <P=2>, 3 <P=6>, 10+x = LITE (stream-only ceiling) of the same P
+//   max_grid: 0 = library default, else cap on workgroups
+int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t umem_size,
+                          const struct xsk_gpu_desc* d_descs, uint32_t n, uint8_t* d_verdicts,
+                          struct xsk_gpu_rec* d_recs, void* d_workspace, void* stream) {
+    if (n == 0) return 0;
+    uint32_t grid = echo_grid(n);
+    if (max_grid) {
+        const uint32_t full = ((n + kTile - 1) / kTile + kWaves - 1) / kWaves;
+        grid = max_grid < full ? max_grid : full;
+    }
+    EchoArgs args;
+    args.umem = (uint8_t*)d_umem;
+    args.umem_size = umem_size;
+    args.descs = d_descs;
+    args.n = n;
+    args.verdicts = d_verdicts;
+    args.recs = d_recs;
+    args.partials = (unsigned long long*)d_workspace;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 g(grid), b(kThreads);
+    switch (variant) {
+        case 0: echo_kernel<4, false><<<g, b, 0, s>>>(args); break;
+        case 1: echo_kernel<8, false><<<g, b, 0, s>>>(args); break;
+        case 2: echo_kernel<2, false><<<g, b, 0, s>>>(args); break;
+        case 3: echo_kernel<6, false><<<g, b, 0, s>>>(args); break;
+        case 4: echo_kernel<4, false, 8><<<g, b, 0, s>>>(args); break;
+        case 5: echo_kernel<2, false, 8><<<g, b, 0, s>>>(args); break;
+        case 6: echo_kernel<8, false, 6><<<g, b, 0, s>>>(args); break;
+        case 21: echo_kernel<4, false, 1, 1><<<g, b, 0, s>>>(args); break;
+        case 22: echo_kernel<4, false, 1, 2><<<g, b, 0, s>>>(args); break;
+        case 24: echo_kernel<4, false, 1, 4><<<g, b, 0, s>>>(args); break;
+        case 27: echo_kernel<4, false, 1, 7><<<g, b, 0, s>>>(args); break;
+        case 50: echo_kernel5<6, 1><<<g, b, 0, s>>>(args); break;
+        case 51: echo_kernel5<3, 1><<<g, b, 0, s>>>(args); break;
+        case 52: echo_kernel5<4, 1><<<g, b, 0, s>>>(args); break;
+        case 53: echo_kernel5<4, 6><<<g, b, 0, s>>>(args); break;
+        case 54: echo_kernel5<3, 6><<<g, b, 0, s>>>(args); break;
+        case 10: echo_kernel<4, true><<<g, b, 0, s>>>(args); break;
+        case 11: echo_kernel<8, true><<<g, b, 0, s>>>(args); break;
+        case 12: echo_kernel<2, true><<<g, b, 0, s>>>(args); break;
+        case 13: echo_kernel<6, true><<<g, b, 0, s>>>(args); break;
+        default: return -EINVAL;
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"
