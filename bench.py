@@ -39,17 +39,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Rehearsal of the N > 1 path on a one-GPU box (never used by the driver): every rank on cuda:0 and a
+# gloo process group (RCCL refuses two ranks on one device).
+SHARE_GPU = os.environ.get("XSK_BENCH_SHARE_GPU") == "1"
+
+
 def dist_setup(gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if SHARE_GPU else int(os.environ.get("LOCAL_RANK", "0"))
     if world != gpus:
         log(f"warning: --gpus {gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if SHARE_GPU:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:  # "nccl" is RCCL on ROCm; it only carries the barrier and the timing/counter reductions
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     return rank, world, local
 
 
@@ -57,7 +65,7 @@ def allreduce(vals, op, world, dev):
     if world == 1:
         return vals
     import torch.distributed as dist
-    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    t = torch.tensor(vals, dtype=torch.float64, device="cpu" if SHARE_GPU else dev)
     dist.all_reduce(t, op=op)
     return t.tolist()
 
@@ -167,6 +175,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also measure the PCIe-inclusive rate")
+    ap.add_argument("--pool-cap", type=int, default=0, help="cap the batch pool (rehearsals on a shared GPU)")
     args = ap.parse_args()
 
     import xsknet_amd as X
@@ -183,6 +192,8 @@ def main():
     free, _ = torch.cuda.mem_get_info(dev)
     per_batch = batch_bytes + n * 16
     pool = max(1, min(W + K, int(free * 0.85) // per_batch - 1))
+    if args.pool_cap:
+        pool = min(pool, args.pool_cap)
     rearm_in_loop = pool < W + K
     log(f"[rank {rank}] {desc}; world {world}; pool {pool} batches of {batch_bytes / 2**30:.2f} GiB"
         + (" (re-arm inside timed loop)" if rearm_in_loop else ""))

@@ -367,3 +367,20 @@ def test_kernel_variants_parity(variant, grid):
     assert (d_verd.cpu().numpy() == v_ref).all()
     assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
     assert (d_umem.cpu().numpy() == ref).all()
+
+
+def test_staged_pipeline_multi_chunk():
+    """A host batch of several staged chunks (two-stream pipeline), mixed frames at a 2 KiB stride."""
+    n = 3 * 32768 + 777
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED0909, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
+        v, r, s = ctx.process(descs)
+    assert (v == v_ref).all()
+    assert (r == r_ref).all()
+    for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        assert int(s[k]) == int(s_ref[k])
+    assert (work == ref).all(), np.nonzero(work != ref)[0][:8]

@@ -10,9 +10,12 @@
  *   ZEROCOPY: the UMEM is registered as mapped pinned memory; the kernel reads and rewrites frames
  *             over PCIe in place.  One launch per batch; nothing but descriptors and results moves.
  *   STAGED:   frames are copied host->device into a device mirror of the UMEM (one strided 2-D copy
- *             when the batch has a uniform frame stride, else the batch's byte span), transformed in
+ *             when the chunk has a uniform frame stride, else the chunk's byte span), transformed in
  *             HBM, and only the 38 rewritten header bytes of TX_REPLY frames are copied back and
- *             scattered into the UMEM — bytes the batch does not own are never written.
+ *             scattered into the UMEM — bytes the batch does not own are never written.  Batches of
+ *             more than one chunk run as a two-stream pipeline: the copy-in of chunk i+1 overlaps the
+ *             kernel and the copy-back of chunk i, and the host scatters chunk i while later chunks
+ *             are still in flight.
  */
 #define _GNU_SOURCE
 #define __HIP_PLATFORM_AMD__ 1
@@ -26,23 +29,28 @@
 int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
                               uint32_t n, uint8_t* d_pack, void* stream);
 
+#define NSTREAMS 2
+#define CHUNK_FRAMES 32768u /* staged pipeline granule: ~49 MB of 1500-B frames per copy-in */
+
 struct xsk_gpu_ctx {
     int device;
     int mode;
     uint8_t* umem;
     uint64_t umem_size;
     uint32_t max_batch;
+    uint32_t max_chunks;
     uint8_t* d_umem; /* mapped alias of umem (ZEROCOPY) or device mirror (STAGED) */
     struct xsk_gpu_desc* d_descs;
     uint8_t* d_verdicts;
     struct xsk_gpu_rec* d_recs;
-    struct xsk_gpu_stats* d_stats;
-    void* d_ws;
+    struct xsk_gpu_stats* d_stats; /* [max_chunks] */
+    void* d_ws[NSTREAMS];
     uint8_t* d_pack;  /* STAGED: [max_batch][48] rewritten headers */
     uint8_t* h_pack;  /* STAGED: pinned host copy of d_pack */
     uint8_t* h_verd;  /* pinned verdict staging */
-    struct xsk_gpu_stats* h_stats;
-    hipStream_t stream;
+    struct xsk_gpu_stats* h_stats; /* [max_chunks] */
+    hipStream_t stream[NSTREAMS];
+    hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
     int registered;
 };
 
@@ -59,19 +67,26 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int s = 0; s < NSTREAMS; s++)
+        if (c->stream[s]) (void)hipStreamSynchronize(c->stream[s]);
     if (c->mode == XSK_GPU_MODE_STAGED && c->d_umem) (void)hipFree(c->d_umem);
     if (c->registered) (void)hipHostUnregister(c->umem);
     (void)hipFree(c->d_descs);
     (void)hipFree(c->d_verdicts);
     (void)hipFree(c->d_recs);
     (void)hipFree(c->d_stats);
-    (void)hipFree(c->d_ws);
+    for (int s = 0; s < NSTREAMS; s++) (void)hipFree(c->d_ws[s]);
     (void)hipFree(c->d_pack);
     if (c->h_pack) (void)hipHostFree(c->h_pack);
     if (c->h_verd) (void)hipHostFree(c->h_verd);
     if (c->h_stats) (void)hipHostFree(c->h_stats);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->done) {
+        for (uint32_t i = 0; i < c->max_chunks; i++)
+            if (c->done[i]) (void)hipEventDestroy(c->done[i]);
+        free(c->done);
+    }
+    for (int s = 0; s < NSTREAMS; s++)
+        if (c->stream[s]) (void)hipStreamDestroy(c->stream[s]);
     free(c);
 }
 
@@ -90,8 +105,9 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
     c->umem = (uint8_t*)umem;
     c->umem_size = umem_size;
     c->max_batch = max_batch;
+    c->max_chunks = mode == XSK_GPU_MODE_STAGED ? (max_batch + CHUNK_FRAMES - 1) / CHUNK_FRAMES : 1;
     TRY(hipSetDevice(device));
-    TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamCreateWithFlags(&c->stream[s], hipStreamNonBlocking));
     TRY(hipHostRegister(umem, umem_size, mode == XSK_GPU_MODE_ZEROCOPY ? hipHostRegisterMapped : hipHostRegisterDefault));
     c->registered = 1;
     if (mode == XSK_GPU_MODE_ZEROCOPY) {
@@ -104,17 +120,24 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
     TRY(hipMalloc((void**)&c->d_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc)));
     TRY(hipMalloc((void**)&c->d_verdicts, max_batch));
     TRY(hipMalloc((void**)&c->d_recs, (size_t)max_batch * sizeof(struct xsk_gpu_rec)));
-    TRY(hipMalloc((void**)&c->d_stats, sizeof(struct xsk_gpu_stats)));
+    TRY(hipMalloc((void**)&c->d_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats)));
     {
-        const size_t ws = xsk_gpu_workspace_size(device, max_batch);
+        const uint32_t per = max_batch < CHUNK_FRAMES || mode == XSK_GPU_MODE_ZEROCOPY ? max_batch : CHUNK_FRAMES;
+        const size_t ws = xsk_gpu_workspace_size(device, per);
         if (ws == 0) {
             rc = -EIO;
             goto out;
         }
-        TRY(hipMalloc(&c->d_ws, ws));
+        for (int s = 0; s < NSTREAMS; s++) TRY(hipMalloc(&c->d_ws[s], ws));
     }
     TRY(hipHostMalloc((void**)&c->h_verd, max_batch, hipHostMallocDefault));
-    TRY(hipHostMalloc((void**)&c->h_stats, sizeof(struct xsk_gpu_stats), hipHostMallocDefault));
+    TRY(hipHostMalloc((void**)&c->h_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats), hipHostMallocDefault));
+    c->done = (hipEvent_t*)calloc(c->max_chunks, sizeof(hipEvent_t));
+    if (!c->done) {
+        rc = -ENOMEM;
+        goto out;
+    }
+    for (uint32_t i = 0; i < c->max_chunks; i++) TRY(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
     *out = c;
     return 0;
 out:
@@ -122,7 +145,7 @@ out:
     return rc;
 }
 
-/* Uniform stride S (>= 64, multiple of 16) when addr[i] = addr[0] + i*S for the whole batch. */
+/* Uniform stride S (>= 64, multiple of 16) when addr[i] = addr[0] + i*S for the whole chunk. */
 static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
     if (n < 2) return 0;
     if (d[1].addr <= d[0].addr) return 0;
@@ -133,8 +156,9 @@ static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
     return s;
 }
 
-static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n) {
-    /* Bytes the kernel may read: [align16(addr), align16(addr)+64) u [addr, addr+len), clipped. */
+/* Copy-in of the bytes the kernel may read for frames d[0..n): [align16(addr), align16(addr)+64) u
+ * [addr, addr+len), clipped to the UMEM. */
+static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n, hipStream_t st) {
     uint64_t lo = UINT64_MAX, hi = 0, width = 0;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t a = d[i].addr;
@@ -152,14 +176,41 @@ static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n) {
     const uint64_t s = uniform_stride(d, n);
     if (s && width <= s && (d[0].addr & ~15ull) + (uint64_t)(n - 1) * s + width <= c->umem_size) {
         const uint64_t base = d[0].addr & ~15ull;
-        if (hipMemcpy2DAsync(c->d_umem + base, s, c->umem + base, s, width, n, hipMemcpyHostToDevice, c->stream) !=
-            hipSuccess)
+        if (hipMemcpy2DAsync(c->d_umem + base, s, c->umem + base, s, width, n, hipMemcpyHostToDevice, st) != hipSuccess)
             return -EIO;
         return 0;
     }
-    if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, c->stream) != hipSuccess)
-        return -EIO;
+    if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, st) != hipSuccess) return -EIO;
     return 0;
+}
+
+/* Enqueue one chunk [i0, i0+n) of the batch on stream st; results land in the pinned host buffers
+ * and c->done[ci] fires when they are there. */
+static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t i0, uint32_t n, uint32_t ci,
+                         int want_recs, int s) {
+    int rc = 0;
+    const hipStream_t st = c->stream[s];
+    struct xsk_gpu_desc* dd = c->d_descs + i0;
+    TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, st));
+    TRY(hipMemsetAsync(c->d_stats + ci, 0, sizeof(struct xsk_gpu_stats), st));
+    if (c->mode == XSK_GPU_MODE_STAGED) {
+        rc = stage_in(c, descs + i0, n, st);
+        if (rc) goto out;
+    }
+    rc = xsk_gpu_echo_dev(c->d_umem, c->umem_size, dd, n, c->d_verdicts + i0, want_recs ? c->d_recs + i0 : NULL,
+                          c->d_stats + ci, c->d_ws[s], st);
+    if (rc) goto out;
+    if (c->mode == XSK_GPU_MODE_STAGED) {
+        rc = xsk_gpu__pack_headers_dev(c->d_umem, dd, c->d_verdicts + i0, n, c->d_pack + (size_t)i0 * 48u, st);
+        if (rc) goto out;
+        TRY(hipMemcpyAsync(c->h_pack + (size_t)i0 * 48u, c->d_pack + (size_t)i0 * 48u, (size_t)n * 48u,
+                           hipMemcpyDeviceToHost, st));
+    }
+    TRY(hipMemcpyAsync(c->h_verd + i0, c->d_verdicts + i0, n, hipMemcpyDeviceToHost, st));
+    TRY(hipMemcpyAsync(c->h_stats + ci, c->d_stats + ci, sizeof *c->h_stats, hipMemcpyDeviceToHost, st));
+    TRY(hipEventRecord(c->done[ci], st));
+out:
+    return rc;
 }
 
 int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
@@ -169,35 +220,38 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
     if (n == 0) return 0;
     if (n > c->max_batch) return -EINVAL;
     TRY(hipSetDevice(c->device));
-    TRY(hipMemcpyAsync(c->d_descs, descs, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, c->stream));
-    TRY(hipMemsetAsync(c->d_stats, 0, sizeof(struct xsk_gpu_stats), c->stream));
-    if (c->mode == XSK_GPU_MODE_STAGED) {
-        rc = stage_in(c, descs, n);
-        if (rc) goto out;
+    const uint32_t chunk = c->mode == XSK_GPU_MODE_STAGED ? CHUNK_FRAMES : n;
+    const uint32_t nchunks = (n + chunk - 1) / chunk;
+    for (uint32_t ci = 0; ci < nchunks; ci++) {
+        const uint32_t i0 = ci * chunk, m = n - i0 < chunk ? n - i0 : chunk;
+        rc = enqueue_chunk(c, descs, i0, m, ci, recs != NULL, (int)(ci % NSTREAMS));
+        if (rc) goto drain;
     }
-    rc = xsk_gpu_echo_dev(c->d_umem, c->umem_size, c->d_descs, n, c->d_verdicts, recs ? c->d_recs : NULL, c->d_stats,
-                          c->d_ws, c->stream);
-    if (rc) goto out;
-    if (c->mode == XSK_GPU_MODE_STAGED) {
-        rc = xsk_gpu__pack_headers_dev(c->d_umem, c->d_descs, c->d_verdicts, n, c->d_pack, c->stream);
-        if (rc) goto out;
-        TRY(hipMemcpyAsync(c->h_pack, c->d_pack, (size_t)n * 48u, hipMemcpyDeviceToHost, c->stream));
-    }
-    TRY(hipMemcpyAsync(c->h_verd, c->d_verdicts, n, hipMemcpyDeviceToHost, c->stream));
-    if (recs) TRY(hipMemcpyAsync(recs, c->d_recs, (size_t)n * sizeof *recs, hipMemcpyDeviceToHost, c->stream));
-    TRY(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof *c->h_stats, hipMemcpyDeviceToHost, c->stream));
-    TRY(hipStreamSynchronize(c->stream));
-    if (c->mode == XSK_GPU_MODE_STAGED) {
-        for (uint32_t i = 0; i < n; i++)
-            if (c->h_verd[i] == XSK_GPU_TX_REPLY) memcpy(c->umem + descs[i].addr, c->h_pack + (size_t)i * 48u, 38);
+    for (uint32_t ci = 0; ci < nchunks; ci++) {
+        const uint32_t i0 = ci * chunk, m = n - i0 < chunk ? n - i0 : chunk;
+        if (hipEventSynchronize(c->done[ci]) != hipSuccess) {
+            rc = -EIO;
+            goto drain;
+        }
+        if (c->mode == XSK_GPU_MODE_STAGED) { /* scatter the rewritten bytes of this chunk's replies */
+            for (uint32_t i = i0; i < i0 + m; i++)
+                if (c->h_verd[i] == XSK_GPU_TX_REPLY) memcpy(c->umem + descs[i].addr, c->h_pack + (size_t)i * 48u, 38);
+        }
+        if (stats) {
+            stats->rx_packets += c->h_stats[ci].rx_packets;
+            stats->rx_bytes += c->h_stats[ci].rx_bytes;
+            stats->tx_packets += c->h_stats[ci].tx_packets;
+            stats->tx_bytes += c->h_stats[ci].tx_bytes;
+        }
     }
     if (verdicts) memcpy(verdicts, c->h_verd, n);
-    if (stats) {
-        stats->rx_packets += c->h_stats->rx_packets;
-        stats->rx_bytes += c->h_stats->rx_bytes;
-        stats->tx_packets += c->h_stats->tx_packets;
-        stats->tx_bytes += c->h_stats->tx_bytes;
+    if (recs) {
+        for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamSynchronize(c->stream[s]));
+        TRY(hipMemcpy(recs, c->d_recs, (size_t)n * sizeof *recs, hipMemcpyDeviceToHost));
     }
+    return 0;
+drain:
+    for (int s = 0; s < NSTREAMS; s++) (void)hipStreamSynchronize(c->stream[s]);
 out:
     return rc;
 }
