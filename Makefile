@@ -20,7 +20,10 @@ $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 $(CSRC)/xsk_gpu_host.o: $(CSRC)/xsk_gpu_host.c include/xsk_gpu.h
 	$(CC) $(CFLAGS) -I$(ROCM)/include -c -o $@ $<
 
-$(LIB): $(HIPOBJ) $(CSRC)/xsk_gpu_host.o
+$(CSRC)/xsk_gpu_rx.o: $(CSRC)/xsk_gpu_rx.c $(CSRC)/xsk_ring.h include/xsk_gpu.h
+	$(CC) $(CFLAGS) -c -o $@ $<
+
+$(LIB): $(HIPOBJ) $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libxsknet_amd.so
 
 tools/echo_replay: tools/echo_replay.c $(LIB) include/xsk_gpu.h

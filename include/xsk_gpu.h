@@ -153,6 +153,65 @@ int xsk_gpu_process(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t
 void xsk_gpu_fini(xsk_gpu_ctx* ctx);
 
 /* ------------------------------------------------------------------------------------------ */
+/* AF_XDP ring loop: the reference's handle_receive_packets() around one xsk_gpu_process().    */
+/* ------------------------------------------------------------------------------------------ */
+
+/* An AF_XDP ring, field-compatible with libxdp's struct xsk_ring_prod / struct xsk_ring_cons
+ * (<xdp/xsk.h>), so a caller passes &xsk->rx, &xsk->tx, &umem->fq, &umem->cq cast to this type.
+ * Descriptor rings (RX, TX) hold struct xsk_gpu_desc entries, address rings (fill, completion)
+ * hold uint64_t UMEM offsets. */
+struct xsk_gpu_ring {
+    uint32_t cached_prod;
+    uint32_t cached_cons;
+    uint32_t mask;
+    uint32_t size;
+    uint32_t* producer;
+    uint32_t* consumer;
+    void* ring;
+    uint32_t* flags;
+};
+
+/* The client's free-frame stack: struct xsk_socket_info's umem_frame_addr[] / umem_frame_free
+ * (src/lib/xsk_utils.h:30-31), popped by xsk_alloc_umem_frame and pushed by xsk_free_umem_frame
+ * (src/lib/xsk_receive.c:54-70). */
+struct xsk_gpu_frame_pool {
+    uint64_t* addr;
+    uint32_t n_free;
+    uint32_t capacity;
+};
+
+struct xsk_gpu_rx_result {
+    uint32_t received;   /* RX descriptors consumed                                     */
+    uint32_t replied;    /* TX_REPLY frames submitted to the TX ring                    */
+    uint32_t tx_full;    /* TX_REPLY frames dropped because the TX ring was full        */
+    uint32_t refilled;   /* free frames handed to the fill ring                         */
+};
+
+#define XSK_GPU_RX_MAX_STEP 1024u /* frames per xsk_gpu_rx_step() call */
+
+/* One pass of handle_receive_packets() (src/lib/xsk_receive.c:192-237) with the transform on the
+ * GPU and the XSK TX path the reference leaves commented out (:174-186) enabled instead of the
+ * per-frame sendto() (:166):
+ *   1. peek up to min(max_batch, XSK_GPU_RX_MAX_STEP) RX descriptors (:196); none -> return 0;
+ *   2. refill the fill ring with min(free fill slots, free frames) frames from `pool` (:201-217;
+ *      the reference reserves the free-slot count even when it has fewer free frames);
+ *   3. xsk_gpu_process() the batch (replaces the per-frame process_packet() loop :220-230);
+ *   4. submit every TX_REPLY frame to the TX ring; a reply that finds the TX ring full is dropped
+ *      and its frame freed, like :178-181; every other frame goes back to `pool` (:226-227);
+ *   5. release the RX entries (:232).
+ * Counters: rx_packets += received (:233), rx_bytes += sum(len) (:229), tx_packets / tx_bytes count
+ * the frames actually submitted (:171-172 count successful sends).  The TX kick (sendto on the XSK
+ * fd, :86) stays with the caller, which owns the socket.  Returns the number of frames received
+ * (0 if the RX ring was empty) or a negative errno; `res` may be NULL. */
+int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ring* fill, struct xsk_gpu_ring* tx,
+                    struct xsk_gpu_frame_pool* pool, uint32_t max_batch, struct xsk_gpu_stats* stats,
+                    struct xsk_gpu_rx_result* res);
+
+/* complete_tx() (src/lib/xsk_receive.c:77-99) minus the kick: move up to `max` completed TX frames
+ * from the completion ring back to `pool`.  Returns the number moved. */
+uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_pool* pool, uint32_t max);
+
+/* ------------------------------------------------------------------------------------------ */
 /* Bench / test utilities (not on the hot path).                                               */
 /* ------------------------------------------------------------------------------------------ */
 

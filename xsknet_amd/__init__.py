@@ -22,7 +22,7 @@ __all__ = [
     "LIB_PATH", "lib", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
-    "MODE_ZEROCOPY", "MODE_STAGED", "timing_enable", "timing_read",
+    "MODE_ZEROCOPY", "MODE_STAGED", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -56,6 +56,25 @@ class XskGpuError(RuntimeError):
         self.rc = rc
 
 
+class Ring(C.Structure):
+    """struct xsk_gpu_ring == libxdp's struct xsk_ring_prod / xsk_ring_cons."""
+    _fields_ = [("cached_prod", C.c_uint32), ("cached_cons", C.c_uint32), ("mask", C.c_uint32),
+                ("size", C.c_uint32), ("producer", C.c_void_p), ("consumer", C.c_void_p), ("ring", C.c_void_p),
+                ("flags", C.c_void_p)]
+
+
+class FramePool(C.Structure):
+    """struct xsk_gpu_frame_pool: the client's free-frame stack (xsk_utils.h:30-31)."""
+    _fields_ = [("addr", C.c_void_p), ("n_free", C.c_uint32), ("capacity", C.c_uint32)]
+
+
+class RxResult(C.Structure):
+    _fields_ = [("received", C.c_uint32), ("replied", C.c_uint32), ("tx_full", C.c_uint32),
+                ("refilled", C.c_uint32)]
+
+
+assert C.sizeof(Ring) == 48 and C.sizeof(FramePool) == 16 and C.sizeof(RxResult) == 16
+
 _lib: Optional[C.CDLL] = None
 
 _P = C.c_void_p
@@ -73,6 +92,9 @@ _SIGS = {
     "xsk_gpu_stream_read_dev": ([_P, C.c_uint64, _P, _P], C.c_int),
     "xsk_gpu_timing_enable": ([C.c_int], C.c_int),
     "xsk_gpu_timing_read": ([C.POINTER(C.c_double), C.POINTER(C.c_uint64)], C.c_int),
+    "xsk_gpu_rx_step": ([_P, C.POINTER(Ring), C.POINTER(Ring), C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32,
+                         _P, C.POINTER(RxResult)], C.c_int),
+    "xsk_gpu_tx_complete": ([C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32], C.c_uint32),
 }
 
 
@@ -169,6 +191,15 @@ class EchoContext:
             self._ctx, descs.ctypes.data, n, verdicts.ctypes.data, recs.ctypes.data if recs is not None else None,
             stats.ctypes.data))
         return verdicts, recs, stats[0]
+
+    def rx_step(self, rx: Ring, fill: Ring, tx: Ring, pool: FramePool, max_batch: int, stats=None):
+        """xsk_gpu_rx_step on this context; returns (received, RxResult)."""
+        res = RxResult()
+        rc = lib().xsk_gpu_rx_step(self._ctx, C.byref(rx), C.byref(fill), C.byref(tx), C.byref(pool), max_batch,
+                                   stats.ctypes.data if stats is not None else None, C.byref(res))
+        if rc < 0:
+            raise XskGpuError("xsk_gpu_rx_step", rc)
+        return rc, res
 
     def close(self) -> None:
         if self._ctx:

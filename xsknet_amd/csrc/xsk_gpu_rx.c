@@ -1,0 +1,96 @@
+/*
+ * xsk_gpu_rx.c — the client's RX loop step (src/lib/xsk_receive.c:192-237) over AF_XDP rings with
+ * the echo transform on the GPU and replies leaving through the XSK TX ring (the reference's
+ * commented-out path :174-186) instead of one sendto() per frame (:166).  Host code (C11).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <string.h>
+
+#include "../../include/xsk_gpu.h"
+#include "xsk_ring.h"
+
+static inline void pool_push(struct xsk_gpu_frame_pool* p, uint64_t a) {
+    if (p->n_free < p->capacity) p->addr[p->n_free++] = a; /* xsk_free_umem_frame (:65-70) */
+}
+
+int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ring* fill, struct xsk_gpu_ring* tx,
+                    struct xsk_gpu_frame_pool* pool, uint32_t max_batch, struct xsk_gpu_stats* stats,
+                    struct xsk_gpu_rx_result* res) {
+    struct xsk_gpu_desc descs[XSK_GPU_RX_MAX_STEP];
+    uint8_t verdict[XSK_GPU_RX_MAX_STEP];
+    struct xsk_gpu_rx_result r = {0, 0, 0, 0};
+    if (!ctx || !rx || !fill || !tx || !pool || !pool->addr || max_batch == 0) return -EINVAL;
+    if (max_batch > XSK_GPU_RX_MAX_STEP) max_batch = XSK_GPU_RX_MAX_STEP;
+
+    uint32_t idx_rx = 0;
+    const uint32_t rcvd = xr_cons_peek(rx, max_batch, &idx_rx); /* :196 */
+    if (!rcvd) {
+        if (res) *res = r;
+        return 0;
+    }
+    /* :201-217 — stock the fill ring from the free-frame stack */
+    uint32_t stock = xr_prod_free(fill, pool->n_free);
+    if (stock > pool->n_free) stock = pool->n_free;
+    if (stock) {
+        uint32_t idx_fq = 0;
+        if (xr_prod_reserve(fill, stock, &idx_fq) == stock) {
+            for (uint32_t i = 0; i < stock; i++) *xr_addr(fill, idx_fq + i) = pool->addr[--pool->n_free];
+            xr_prod_submit(fill, stock);
+            r.refilled = stock;
+        }
+    }
+    /* :222-223 — the batch's descriptors */
+    for (uint32_t i = 0; i < rcvd; i++) descs[i] = *xr_desc(rx, idx_rx + i);
+
+    struct xsk_gpu_stats st;
+    memset(&st, 0, sizeof st);
+    const int rc = xsk_gpu_process(ctx, descs, rcvd, verdict, NULL, &st);
+    if (rc) { /* frames stay on the RX ring (not released); the caller may retry or tear down */
+        rx->cached_cons -= rcvd;
+        return rc;
+    }
+    uint32_t nrep = 0;
+    for (uint32_t i = 0; i < rcvd; i++) nrep += verdict[i] == XSK_GPU_TX_REPLY;
+    /* :174-186 — replies onto the TX ring, as many as it has room for */
+    uint32_t idx_tx = 0, room = 0;
+    if (nrep) {
+        room = xr_prod_free(tx, nrep);
+        if (room > nrep) room = nrep;
+        if (room) xr_prod_reserve(tx, room, &idx_tx);
+    }
+    uint64_t tx_bytes = 0;
+    for (uint32_t i = 0; i < rcvd; i++) {
+        if (verdict[i] == XSK_GPU_TX_REPLY && r.replied < room) {
+            struct xsk_gpu_desc* t = xr_desc(tx, idx_tx + r.replied);
+            t->addr = descs[i].addr;
+            t->len = descs[i].len;
+            t->options = 0;
+            r.replied++;
+            tx_bytes += descs[i].len;
+        } else {
+            if (verdict[i] == XSK_GPU_TX_REPLY) r.tx_full++;
+            pool_push(pool, descs[i].addr); /* :226-227 */
+        }
+    }
+    if (r.replied) xr_prod_submit(tx, r.replied);
+    xr_cons_release(rx, rcvd); /* :232 */
+    r.received = rcvd;
+    if (stats) {
+        stats->rx_packets += rcvd;       /* :233 */
+        stats->rx_bytes += st.rx_bytes;  /* :229 */
+        stats->tx_packets += r.replied;  /* :172 */
+        stats->tx_bytes += tx_bytes;     /* :171 */
+    }
+    if (res) *res = r;
+    return (int)rcvd;
+}
+
+uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_pool* pool, uint32_t max) {
+    if (!comp || !pool || !pool->addr || max == 0) return 0;
+    uint32_t idx = 0;
+    const uint32_t n = xr_cons_peek(comp, max, &idx); /* :89 */
+    for (uint32_t i = 0; i < n; i++) pool_push(pool, *xr_addr(comp, idx + i)); /* :94-95 */
+    if (n) xr_cons_release(comp, n); /* :97 */
+    return n;
+}
