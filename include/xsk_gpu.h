@@ -153,6 +153,32 @@ int xsk_gpu_process(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t
 void xsk_gpu_fini(xsk_gpu_ctx* ctx);
 
 /* ------------------------------------------------------------------------------------------ */
+/* XDP ingress filter on the device (the frames the echo transform sees).                      */
+/* ------------------------------------------------------------------------------------------ */
+
+/* XDP actions, values of enum xdp_action (<linux/bpf.h>). */
+#define XSK_GPU_XDP_DROP 1
+#define XSK_GPU_XDP_PASS 2
+#define XSK_GPU_XDP_REDIRECT 4
+
+/* Bytes of zero-or-garbage device workspace xsk_gpu_classify_dev() needs for n frames. */
+size_t xsk_gpu_classify_workspace_size(uint32_t n);
+
+/* xdp_sock_prog() of src/kern/inner_xdp.c:26-61 over a device-resident batch (phy_xdp.c:39-81 makes
+ * the same tests with a devmap instead of the xsks_map):
+ *   d_actions[i] = XSK_GPU_XDP_DROP      if len < 14                        (:35-36)
+ *                  XSK_GPU_XDP_PASS      if bytes 12-13 != 08 00            (:38-39)
+ *                  XSK_GPU_XDP_DROP      if len < 34                        (:41-42)
+ *                  XSK_GPU_XDP_PASS      if byte 23 != 1 (not ICMP)         (:44-45)
+ *                  XSK_GPU_XDP_REDIRECT  if target_bound, else XSK_GPU_XDP_DROP (:57-60)
+ * (a descriptor outside the UMEM is XSK_GPU_XDP_DROP: build-added).  With d_out (16-B aligned, room
+ * for n descriptors) the REDIRECT frames' descriptors are also written there in batch order and
+ * their count to *d_nout: the input of xsk_gpu_echo_dev().  Asynchronous on `stream`. */
+int xsk_gpu_classify_dev(const void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                         int target_bound, uint8_t* d_actions, struct xsk_gpu_desc* d_out, uint32_t* d_nout,
+                         void* d_workspace, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
 /* AF_XDP ring loop: the reference's handle_receive_packets() around one xsk_gpu_process().    */
 /* ------------------------------------------------------------------------------------------ */
 

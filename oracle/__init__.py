@@ -58,6 +58,8 @@ def lib() -> C.CDLL:
                                     C.c_uint64, C.c_int, C.c_uint32, C.c_uint32], C.c_int),
             "oracle_rearm": ([_P, _P, _P, C.c_uint32], None),
             "oracle_mix64": ([C.c_uint64], C.c_uint64),
+            "oracle_xdp_classify": ([_P, C.c_uint32, C.c_int], C.c_int),
+            "oracle_xdp_classify_batch": ([_P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P], C.c_uint32),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -122,3 +124,20 @@ def rearm(umem: np.ndarray, descs: np.ndarray, verdicts: np.ndarray) -> None:
 
 def mix64(x: int) -> int:
     return lib().oracle_mix64(x)
+
+
+XDP_DROP, XDP_PASS, XDP_REDIRECT = 1, 2, 4
+
+
+def xdp_classify(frame: np.ndarray, length: int, target_bound: bool = True) -> int:
+    return lib().oracle_xdp_classify(frame.ctypes.data, length, 1 if target_bound else 0)
+
+
+def xdp_classify_batch(umem: np.ndarray, descs: np.ndarray, target_bound: bool = True):
+    """inner_xdp.c:26-61 over a batch: (actions, redirected descriptors in order)."""
+    n = len(descs)
+    actions = np.zeros(n, np.uint8)
+    out = np.zeros(max(n, 1), DESC_DTYPE)
+    k = lib().oracle_xdp_classify_batch(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, 1 if target_bound else 0,
+                                        actions.ctypes.data, out.ctypes.data)
+    return actions, out[:k]

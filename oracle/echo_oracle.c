@@ -319,3 +319,31 @@ void oracle_rearm(uint8_t* umem, const struct xsk_gpu_desc* descs, const uint8_t
         st_le16(p + 36, c);
     }
 }
+
+/* ---------------------------------------------------------------------------------------------- */
+/* XDP ingress filter (src/kern/inner_xdp.c:26-61; phy_xdp.c:39-81 applies the same tests)         */
+/* ---------------------------------------------------------------------------------------------- */
+
+int oracle_xdp_classify(const uint8_t* pkt, uint32_t len, int target_bound) {
+    if (len < 14) return 1;                  /* OVER(eth, data_end) -> XDP_DROP, :35-36            */
+    if (ld_be16(pkt + 12) != 0x0800) return 2; /* eth->h_proto != htons(ETH_P_IP) -> XDP_PASS, :38 */
+    if (len < 34) return 1;                  /* OVER(iph, data_end) -> XDP_DROP, :41-42            */
+    if (pkt[23] != 1) return 2;              /* iph->protocol != IPPROTO_ICMP -> XDP_PASS, :44-45  */
+    return target_bound ? 4 : 1;             /* bpf_redirect_map if the queue is bound, :57-60     */
+}
+
+uint32_t oracle_xdp_classify_batch(const uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs,
+                                   uint32_t n, int target_bound, uint8_t* actions, struct xsk_gpu_desc* redirect) {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t a = descs[i].addr;
+        const uint32_t len = descs[i].len;
+        const uint32_t need = len < 34 ? (len < 14 ? 0 : 14) : 34;
+        int act;
+        if (len > XSK_GPU_MAX_LEN || a > umem_size || need > umem_size - a) act = 1;
+        else act = oracle_xdp_classify(umem + a, len, target_bound);
+        actions[i] = (uint8_t)act;
+        if (act == 4) redirect[k++] = descs[i];
+    }
+    return k;
+}

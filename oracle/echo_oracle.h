@@ -60,6 +60,18 @@ void oracle_rearm(uint8_t* umem, const struct xsk_gpu_desc* descs, const uint8_t
 
 uint64_t oracle_mix64(uint64_t x);
 
+/* xdp_sock_prog() of src/kern/inner_xdp.c:26-61 (the same tests as xdp_redirect() of
+ * src/kern/phy_xdp.c:39-81) on one frame of `len` bytes: XDP_DROP (1) if len < 14 (:35-36),
+ * XDP_PASS (2) if the ethertype is not IPv4 (:38-39), XDP_DROP if len < 34 (:41-42), XDP_PASS if the
+ * IP protocol is not ICMP (:44-45), else XDP_REDIRECT (4) when a target is bound (xsks_map entry
+ * :57-58 / devmap ifindex) and XDP_DROP when none is (:60). */
+int oracle_xdp_classify(const uint8_t* pkt, uint32_t len, int target_bound);
+
+/* Batch form: actions[n]; redirect[] receives the REDIRECT descriptors in order; returns their count.
+ * A descriptor outside the UMEM is XDP_DROP (build-added: the kernel's data/data_end never are). */
+uint32_t oracle_xdp_classify_batch(const uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs,
+                                   uint32_t n, int target_bound, uint8_t* actions, struct xsk_gpu_desc* redirect);
+
 #ifdef __cplusplus
 }
 #endif

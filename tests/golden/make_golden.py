@@ -19,6 +19,8 @@ ships no tests or fixtures.  The vectors here are therefore pinn
    written in the network-order formulation (not the C oracle's little-endian u16 code path).
 
 The C oracle (oracle/echo_oracle.c) and the GPU kernel are both checked against these files.
+classify.json holds the XDP ingress-filter action (src/kern/inner_xdp.c:26-61) of every frame, with
+and without a bound AF_XDP socket, from a separate restatement (xdp_classify below).
 """
 import json
 import os
@@ -80,6 +82,19 @@ def transform(frame: bytes, length: int):
     rec["verdict"] = verdict
     rec["icmp_csum_out"] = (b[36] << 8) | b[37]
     return bytes(b), rec
+
+
+def xdp_classify(frame: bytes, length: int, bound: bool) -> int:
+    """Independent restatement of xdp_sock_prog (src/kern/inner_xdp.c:26-61): 1 DROP, 2 PASS, 4 REDIRECT."""
+    if length < 14:  # OVER(eth, data_end)
+        return 1
+    if frame[12:14] != b"\x08\x00":
+        return 2
+    if length < 34:  # OVER(iph, data_end)
+        return 1
+    if frame[23] != 1:
+        return 2
+    return 4 if bound else 1
 
 
 def build_frame(length, *, dst=bytes.fromhex("020000000001"), src=bytes.fromhex("020000000002"),
@@ -155,6 +170,10 @@ def main():
         vectors.append(dict(name=name, len=length, input=frame.hex(), output=out.hex(), rec=rec))
     with open(os.path.join(HERE, "frames.json"), "w") as f:
         json.dump(vectors, f, indent=1)
+    classify = [dict(name=name, len=length, bound=xdp_classify(frame, length, True),
+                     unbound=xdp_classify(frame, length, False)) for name, length, frame in frames()]
+    with open(os.path.join(HERE, "classify.json"), "w") as f:
+        json.dump(classify, f, indent=1)
 
     kat = {
         "rfc1071_example": {"bytes": "0001f203f4f5f6f7", "folded_sum": 0xDDF2, "checksum": 0x220D},

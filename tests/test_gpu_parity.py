@@ -384,3 +384,84 @@ def test_staged_pipeline_multi_chunk():
     for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
         assert int(s[k]) == int(s_ref[k])
     assert (work == ref).all(), np.nonzero(work != ref)[0][:8]
+
+
+# ---- XDP ingress filter (inner_xdp.c:26-61) on the device ------------------------------------------
+def gpu_classify(umem, descs, bound):
+    dev = _dev()
+    n = len(descs)
+    d_umem = to_dev(umem)
+    d_descs = to_dev(np.ascontiguousarray(descs, X.DESC_DTYPE))
+    act = torch.full((max(n, 1),), 0xEE, dtype=torch.uint8, device=dev)
+    out = torch.zeros(max(n, 1) * 16, dtype=torch.uint8, device=dev)
+    nout = torch.full((1,), 0xFFFFFFFF, dtype=torch.int64, device=dev)
+    X.classify_dev(d_umem, d_descs, n, bound, act, out, nout)
+    torch.cuda.synchronize()
+    k = int(nout.cpu().numpy().view(np.uint32)[0])
+    return act.cpu().numpy()[:n], out.cpu().numpy().view(X.DESC_DTYPE)[:k]
+
+
+@pytest.mark.parametrize("bound", [True, False])
+@pytest.mark.parametrize("n,lo,hi,stride", [(1, 0, 200, 256), (255, 0, 200, 256), (257, 0, 200, 256),
+                                            (100000, 0, 1500, 1536), (70000, 64, 64, 64)])
+def test_classify_parity(n, lo, hi, stride, bound):
+    umem = np.zeros(n * stride, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, stride, seed=0x5EED0C0C + n, mode=1, len_lo=lo, len_hi=hi)
+    a_ref, r_ref = oracle.xdp_classify_batch(umem, descs, bound)
+    a, r = gpu_classify(umem, descs, bound)
+    assert (a == a_ref).all(), np.nonzero(a != a_ref)[0][:8]
+    assert len(r) == len(r_ref) and (r == r_ref).all()
+
+
+def test_classify_golden_and_bad_descriptors():
+    import json
+    cls = {c["name"]: c for c in json.load(open(os.path.join(ROOT, "tests", "golden", "classify.json")))}
+    vecs = golden_frames()
+    stride = 2048
+    umem = np.zeros(len(vecs) * stride, np.uint8)
+    descs = np.zeros(len(vecs) + 3, X.DESC_DTYPE)
+    for i, v in enumerate(vecs):
+        fr = np.frombuffer(bytes.fromhex(v["input"]), np.uint8)
+        umem[i * stride + 3:i * stride + 3 + len(fr)] = fr  # odd start
+        descs[i] = (i * stride + 3, v["len"], 0)
+    descs[len(vecs)] = (umem.nbytes - 20, 34, 0)      # IPv4 header would cross the UMEM end
+    descs[len(vecs) + 1] = (umem.nbytes + 5, 64, 0)   # outside
+    descs[len(vecs) + 2] = (umem.nbytes - 13, 13, 0)  # short, inside: DROP by the length test
+    a, r = gpu_classify(umem, descs, True)
+    for i, v in enumerate(vecs):
+        assert a[i] == cls[v["name"]]["bound"], v["name"]
+    assert list(a[len(vecs):]) == [1, 1, 1]
+    a_ref, r_ref = oracle.xdp_classify_batch(umem, descs, True)
+    assert (a == a_ref).all() and (r == r_ref).all()
+
+
+def test_classify_then_echo_pipeline():
+    """Filter a mixed 1 M batch on the device, transform only the redirected frames, compare with the
+    CPU filter + oracle transform on sampled frames and on the counters."""
+    dev = _dev()
+    n, stride = 1 << 20, 2048
+    d_umem = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    X.synth_dev(d_umem, d_descs, n, 0, stride, 0x5EED0D0D, 0, 1, 1, 20, 1500)
+    host = d_umem.cpu().numpy()
+    descs = d_descs.cpu().numpy().view(X.DESC_DTYPE)
+    act = torch.empty(n, dtype=torch.uint8, device=dev)
+    red = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    nred = torch.zeros(1, dtype=torch.int64, device=dev)
+    X.classify_dev(d_umem, d_descs, n, True, act, red, nred)
+    torch.cuda.synchronize()
+    k = int(nred.cpu().numpy().view(np.uint32)[0])
+    a_ref, r_ref = oracle.xdp_classify_batch(host, descs, True)
+    assert (act.cpu().numpy() == a_ref).all() and k == len(r_ref)
+    stats = torch.zeros(40, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(X.workspace_size(0, k), dtype=torch.uint8, device=dev)
+    verd = torch.empty(k, dtype=torch.uint8, device=dev)
+    X.echo_dev(d_umem, red, k, verd, None, stats, ws)
+    torch.cuda.synchronize()
+    ref = host.copy()
+    v_ref, _, s_ref = oracle.echo_batch(ref, r_ref, threads=8)
+    assert (verd.cpu().numpy() == v_ref).all()
+    st = stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    for key in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        assert int(st[key]) == int(s_ref[key])
+    assert (d_umem.cpu().numpy() == ref).all()

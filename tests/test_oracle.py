@@ -151,3 +151,32 @@ def test_mt_matches_single_thread():
     v1, r1, s1 = oracle.echo_batch(u1, descs)
     v2, r2, s2 = oracle.echo_batch(u2, descs, threads=4)
     assert (v1 == v2).all() and (r1 == r2).all() and s1 == s2 and (u1 == u2).all()
+
+
+def test_xdp_classify_golden():
+    """oracle_xdp_classify (inner_xdp.c:26-61) against the independent restatement's actions."""
+    import json
+    import os
+    from tests.conftest import ROOT
+    cls = {c["name"]: c for c in json.load(open(os.path.join(ROOT, "tests", "golden", "classify.json")))}
+    for vec in golden_frames():
+        f = np.frombuffer(bytes.fromhex(vec["input"]), np.uint8).copy()
+        c = cls[vec["name"]]
+        assert oracle.xdp_classify(f, vec["len"], True) == c["bound"], vec["name"]
+        assert oracle.xdp_classify(f, vec["len"], False) == c["unbound"], vec["name"]
+
+
+def test_xdp_classify_batch_compacts_in_order():
+    n = 3000
+    umem = np.zeros(n * 256, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 256, seed=21, mode=1, len_lo=0, len_hi=200)
+    act, red = oracle.xdp_classify_batch(umem, descs, True)
+    assert set(np.unique(act)) <= {1, 2, 4} and (act == 4).any() and (act == 2).any() and (act == 1).any()
+    assert (red == descs[act == 4]).all()
+    act0, red0 = oracle.xdp_classify_batch(umem, descs, False)
+    assert len(red0) == 0 and ((act0 == 1) == ((act == 1) | (act == 4))).all()
+    # every frame of >= 34 B the echo transform would accept is one the filter redirects; the filter
+    # drops 20..33-B frames (inner_xdp.c:41-42) that process_packet's len >= 20 gate would accept
+    v, _, _ = oracle.echo_batch(umem.copy(), descs)
+    assert (act[(v == 0) & (descs["len"] >= 34)] == 4).all()
+    assert (act[(v == 0) & (descs["len"] < 34)] == 1).all()

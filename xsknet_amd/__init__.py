@@ -23,6 +23,7 @@ __all__ = [
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
     "MODE_ZEROCOPY", "MODE_STAGED", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
+    "classify_dev", "XDP_DROP", "XDP_PASS", "XDP_REDIRECT",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -95,6 +96,8 @@ _SIGS = {
     "xsk_gpu_rx_step": ([_P, C.POINTER(Ring), C.POINTER(Ring), C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32,
                          _P, C.POINTER(RxResult)], C.c_int),
     "xsk_gpu_tx_complete": ([C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32], C.c_uint32),
+    "xsk_gpu_classify_workspace_size": ([C.c_uint32], C.c_size_t),
+    "xsk_gpu_classify_dev": ([_P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, _P, _P], C.c_int),
 }
 
 
@@ -141,6 +144,20 @@ def echo_dev(umem, descs, n: int, verdicts=None, recs=None, stats=None, workspac
     _check("xsk_gpu_echo_dev", lib().xsk_gpu_echo_dev(
         _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, _ptr(verdicts), _ptr(recs), _ptr(stats),
         _ptr(workspace), _stream_ptr(stream)))
+
+
+XDP_DROP, XDP_PASS, XDP_REDIRECT = 1, 2, 4
+
+
+def classify_dev(umem, descs, n: int, bound: bool, actions, out=None, nout=None, workspace=None, stream=None) -> None:
+    """xsk_gpu_classify_dev: the XDP ingress filter (inner_xdp.c:26-61) + in-order compaction."""
+    if workspace is None:
+        import torch
+        workspace = torch.empty(int(lib().xsk_gpu_classify_workspace_size(max(n, 1))), dtype=torch.uint8,
+                                device=umem.device)
+    _check("xsk_gpu_classify_dev", lib().xsk_gpu_classify_dev(
+        _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, 1 if bound else 0, _ptr(actions), _ptr(out),
+        _ptr(nout), _ptr(workspace), _stream_ptr(stream)))
 
 
 def synth_dev(umem, descs, n: int, base_off: int, stride: int, seed: int, first: int = 0, step: int = 1,
