@@ -465,3 +465,69 @@ def test_classify_then_echo_pipeline():
     for key in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
         assert int(st[key]) == int(s_ref[key])
     assert (d_umem.cpu().numpy() == ref).all()
+
+
+def test_more_tiles_than_grid():
+    """4.5 M packed 64-B frames: more tiles than the 16 384-workgroup grid cap, so waves loop."""
+    dev = _dev()
+    n, stride = 4_500_000, 64
+    d_umem = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+    d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    X.synth_dev(d_umem, d_descs, n, 0, stride, 0x5EED1111, 0, 1, 0, 64, 64)
+    before = d_umem.clone()
+    verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    stats = torch.zeros(40, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(X.workspace_size(0, n), dtype=torch.uint8, device=dev)
+    X.echo_dev(d_umem, d_descs, n, verd, recs, stats, ws)
+    torch.cuda.synchronize()
+    st = stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    assert int(st["rx_packets"]) == n and int(st["tx_packets"]) == n and int(st["tx_bytes"]) == 64 * n
+    assert bool((verd == 0).all()) and bool((recs.view(-1, 16)[:, 1] == 3).all())
+    idx = np.sort(np.random.default_rng(3).choice(n, 256, replace=False))
+    idx[-1] = n - 1
+    got = d_umem.view(-1, stride)[torch.from_numpy(idx).to(dev)].cpu().numpy()
+    for k, j in enumerate(idx):
+        L, buf = oracle.synth_frame(0x5EED1111, int(j), 0, 64, 64, cap=64)
+        frame = buf[:64].copy()
+        d1 = np.zeros(1, oracle.DESC_DTYPE)
+        d1[0] = (0, L, 0)
+        oracle.echo_batch(frame, d1)
+        assert (got[k] == frame).all(), j
+    X.rearm_dev(d_umem, d_descs, verd, n)
+    torch.cuda.synchronize()
+    assert torch.equal(before, d_umem)
+
+
+def test_tile_spanning_more_than_2gib():
+    """Frames of one tile more than 2 GiB apart (the kernel's 64-bit-address path)."""
+    dev = _dev()
+    size = (2 << 30) + (512 << 20)  # 2.5 GiB UMEM
+    far = (2 << 30) + (64 << 20)
+    n = 200
+    tmp = np.zeros(n * 2048, np.uint8)
+    src = oracle.synth_batch(tmp, n, 0, 2048, seed=0x5EED1212, mode=1, len_lo=20, len_hi=1500)
+    d_umem = torch.zeros(size, dtype=torch.uint8, device=dev)
+    descs = np.zeros(n, X.DESC_DTYPE)
+    for i in range(n):
+        a = (far if i % 2 else 0) + i * 2048 + (i % 5)
+        d_umem[a:a + 2048] = torch.from_numpy(tmp[i * 2048:(i + 1) * 2048]).to(dev)
+        descs[i] = (a, src[i]["len"], 0)
+    d_descs = to_dev(descs)
+    lo_before = d_umem[:n * 2048 + 64].cpu().numpy().copy()
+    hi_before = d_umem[far:far + n * 2048 + 64].cpu().numpy().copy()
+    verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    X.echo_dev(d_umem, d_descs, n, verd, recs)
+    torch.cuda.synchronize()
+    # oracle on a compact host image: both regions, same relative layout
+    img = np.zeros(2 * (n * 2048 + 64), np.uint8)
+    img[:n * 2048 + 64] = lo_before
+    img[n * 2048 + 64:] = hi_before
+    hd = descs.copy()
+    hd["addr"] = np.where(np.arange(n) % 2 == 1, descs["addr"] - far + n * 2048 + 64, descs["addr"])
+    v_ref, r_ref, _ = oracle.echo_batch(img, hd)
+    assert (verd.cpu().numpy() == v_ref).all()
+    assert (recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+    assert (d_umem[:n * 2048 + 64].cpu().numpy() == img[:n * 2048 + 64]).all()
+    assert (d_umem[far:far + n * 2048 + 64].cpu().numpy() == img[n * 2048 + 64:]).all()
