@@ -15,6 +15,20 @@
 //   mode 9: header read only, 64 B per frame (4 lanes), no payload
 //   mode 10: + 64 B per frame of constant data stored right after the frame's loads are ISSUED
 //            (before they return): the write reaches the DRAM page the reads just opened
+//   mode 11: + 128 B per frame (the whole first line), deferred to the end of the tile (LDS-staged)
+//   mode 12: mode 0, then a second launch that re-reads and rewrites every frame's 64-B window
+//            (two-phase: the whole read stream first, all header writes after it)
+//   mode 13: the second launch of mode 12 alone (64-B window read + write, cold)
+//   mode 14: mode 12 with the 64-B window loaded with the default (cacheable) policy in the first pass
+//   mode 15: phase-separated rounds: a persistent grid (one 1024-thread workgroup per CU) reads 2048
+//            frames per workgroup per round, holding their 64-B windows in LDS (128 KiB), then all
+//            workgroups write their windows back at once; the read stream never meets a write
+//   mode 16: mode 15 without the write phase (the structure's read rate)
+//   mode 17: mode 15 with tiles interleaved across workgroups (step s of every workgroup reads one
+//            compact front of consecutive frames), mode 18: mode 17 without the write phase
+//   mode 19/20: mode 15/16 with two steps (8 frames, 12 loads per lane) in flight per wave
+//   mode 21/22: mode 15/16 with 1024-frame rounds (64 KiB LDS, two workgroups per CU: grid 512)
+//   mode 23/24: mode 21/22 with two steps in flight
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,6 +39,7 @@ template <int MODE>
 __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
                                                    unsigned long long* out, uint8_t* side) {
     __shared__ __attribute__((aligned(16))) uint8_t s_row[4][64 * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t s_row2[MODE == 11 ? 4 : 1][MODE == 11 ? 64 * 128 : 16];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 4, k = lane & 15u;
     const uint32_t ntiles = (n + 63) / 64, nw = gridDim.x * 4;
@@ -53,7 +68,7 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
                     const uint32_t ro = 256u * u + 16u * k;
                     v[u] = u32x4{0, 0, 0, 0};
                     if (ro < len) {
-                        if (MODE == 6) v[u] = *(const u32x4*)(fr + ro);
+                        if (MODE == 6 || (MODE == 14 && u == 0 && k < 4)) v[u] = *(const u32x4*)(fr + ro);
                         else v[u] = __builtin_nontemporal_load((const u32x4*)(fr + ro));
                     }
                 }
@@ -77,6 +92,7 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
             }
             if (MODE == 8 && k < 4) *(u32x4*)(side + (uint64_t)f * 64 + 16u * k) = v[0];
             if ((MODE == 4 || MODE == 7) && k < 4) *(u32x4*)(&s_row[wave][(4 * s + q) * 64 + 16 * k]) = v[0];
+            if (MODE == 11 && k < 8) *(u32x4*)(&s_row2[wave][(4 * s + q) * 128 + 16 * k]) = v[0];
         }
         if (MODE == 4 || MODE == 7) {
             __builtin_amdgcn_wave_barrier();
@@ -92,8 +108,93 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
             }
             __builtin_amdgcn_wave_barrier();
         }
+        if (MODE == 11) {
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const uint32_t f = t * 64 + r * 8 + (lane >> 3);
+                if (f < n) {
+                    u32x4* dst = (u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 7u));
+                    *dst = *(const u32x4*)(&s_row2[wave][(r * 8 + (lane >> 3)) * 128 + 16 * (lane & 7u)]);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
     }
     if (acc == 0x123456789ull) out[0] = acc;  // keeps the loads alive
+}
+
+// Second pass of modes 12-14: 4 lanes per frame re-read the 64-B window and store it back.
+__global__ __launch_bounds__(256) void wexp_patch(uint8_t* buf, uint32_t n, uint32_t stride) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t f = i >> 2, k = i & 3u;
+    if (f >= n) return;
+    u32x4* p = (u32x4*)(buf + (uint64_t)f * stride + 16u * k);
+    u32x4 v = *p;
+    v.x ^= 0u;
+    asm volatile("" : "+v"(v));
+    *p = v;
+}
+
+// Modes 15/16.  grid = workgroups (normally one per CU), 1024 threads each, 2048 frames per round.
+template <bool WRITE, bool IL, uint32_t R = 2048, int ST = 1>
+__global__ __launch_bounds__(1024) void wexp_rounds(uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
+                                                    unsigned long long* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[R * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    const uint32_t per = IL ? R : (n + gridDim.x - 1) / gridDim.x;
+    const uint32_t G = gridDim.x;
+    const uint32_t nrounds = IL ? (n + G * R - 1) / (G * R) : 1u;
+    uint64_t acc = 0;
+    const uint64_t t_start = wall_clock64();
+    for (uint32_t rr = 0; rr < nrounds; ++rr)
+    for (uint32_t r0 = IL ? 0u : blockIdx.x * per, f0 = r0, f1 = IL ? R : min(n, f0 + per); r0 < f1; r0 += R) {
+        // frame of local index j (0..R-1) in this round
+        auto gf = [&](uint32_t j) -> uint32_t {
+            return IL ? (rr * G * (R / 64) + (j >> 6) * G + blockIdx.x) * 64u + (j & 63u) : r0 + j;
+        };
+        // read phase: wave w takes frames r0 + 4*(w + 16*s) + q
+        for (uint32_t s0 = 0; s0 < R / 64; s0 += ST) {
+            u32x4 v[ST][6];
+#pragma unroll
+            for (int t = 0; t < ST; ++t) {
+                const uint32_t j = 4u * (wave + 16u * (s0 + t)) + q;
+                const uint32_t f = gf(j);
+                const bool live = IL ? f < n : f < f1;
+                const uint8_t* fr = buf + (uint64_t)(live ? f : 0u) * stride;
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+                    const uint32_t ro = 256u * u + 16u * k;
+                    v[t][u] = (live && ro < len) ? __builtin_nontemporal_load((const u32x4*)(fr + ro)) : u32x4{0, 0, 0, 0};
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < ST; ++t) {
+                const uint32_t j = 4u * (wave + 16u * (s0 + t)) + q;
+#pragma unroll
+                for (int u = 0; u < 6; ++u) acc += (uint64_t)v[t][u].x + v[t][u].y + v[t][u].z + v[t][u].w;
+                if (WRITE && k < 4) *(u32x4*)(&s_win[j * 64 + 16 * k]) = v[t][0];
+            }
+        }
+        if (WRITE) {
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < (int)(R * 4 / 1024); ++r) {
+                const uint32_t idx = (uint32_t)r * 1024u + threadIdx.x;  // 16-B piece
+                const uint32_t j = idx >> 2, kk = idx & 3u;
+                const uint32_t f = gf(j);
+                if (IL ? f < n : f < f1) *(u32x4*)(buf + (uint64_t)f * stride + 16u * kk) = *(const u32x4*)(&s_win[j * 64 + 16 * kk]);
+            }
+            __syncthreads();
+        }
+    }
+    if (acc == 0x123456789ull) out[0] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0 && gridDim.x <= 2048) {
+        out[8 + 2 * blockIdx.x] = t_start;
+        out[9 + 2 * blockIdx.x] = wall_clock64();
+    }
 }
 
 extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32_t len, void* out, uint32_t grid,
@@ -115,6 +216,22 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 8: wexp_kernel<8><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 9: wexp_kernel<9><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 10: wexp_kernel<10><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
+        case 11: wexp_kernel<11><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
+        case 12: wexp_kernel<0><<<g, b, 0, s>>>(p, n, stride, len, o, side);
+                 wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
+        case 15: wexp_rounds<true, false><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 16: wexp_rounds<false, false><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 17: wexp_rounds<true, true><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 18: wexp_rounds<false, true><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 19: wexp_rounds<true, false, 2048, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 20: wexp_rounds<false, false, 2048, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 21: wexp_rounds<true, false, 1024, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 22: wexp_rounds<false, false, 1024, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 23: wexp_rounds<true, false, 1024, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 24: wexp_rounds<false, false, 1024, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 13: wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
+        case 14: wexp_kernel<14><<<g, b, 0, s>>>(p, n, stride, len, o, side);
+                 wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -27,7 +27,7 @@ def main():
     free, _ = torch.cuda.mem_get_info(dev)
     pool = max(1, min(int(os.environ.get("WEXP_POOL", "10")), int(free * 0.8) // (n * stride)))
     bufs = [torch.randint(0, 255, (n * stride,), dtype=torch.uint8, device=dev) for _ in range(pool)]
-    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    out = torch.zeros(8 + 2 * 4096, dtype=torch.int64, device=dev)
     side = torch.zeros(n * 64, dtype=torch.uint8, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
     res = {}
@@ -41,6 +41,15 @@ def main():
                     e1.record()
                     if rep:
                         res.setdefault((m, g), []).append((e0, e1))
+                    if rep == 3 and b is bufs[-1] and m in (15, 16, 19, 20, 21, 22) and os.environ.get("WEXP_WG"):
+                        torch.cuda.synchronize()
+                        t = out[8:8 + 2 * g].cpu().view(g, 2).double() / 100.0  # wall_clock64: 100 MHz -> us
+                        t0 = t[:, 0].min()
+                        st, en = (t[:, 0] - t0), (t[:, 1] - t0)
+                        xcd = [round(float(en[x::8].mean()), 1) for x in range(8)]
+                        print(json.dumps({"mode": m, "grid": g, "start_max": round(float(st.max()), 1),
+                                          "end_min": round(float(en.min()), 1), "end_med": round(float(en.median()), 1),
+                                          "end_max": round(float(en.max()), 1), "end_mean_per_xcd": xcd}), flush=True)
         torch.cuda.synchronize()
     for (m, g), evs in sorted(res.items()):
         ts = sorted(a.elapsed_time(b) for a, b in evs)

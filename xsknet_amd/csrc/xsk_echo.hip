@@ -1,5 +1,5 @@
 // xsk_echo.hip — the product entry point of the gfx950 ICMP-echo transform: xsk_gpu_echo_dev() (one
-// launch of echo_kernel5 + the counter fold), the workspace query, the kernel timer the bench reads,
+// launch of the round kernel echo_kernel6 + the counter fold), the workspace query, the kernel timer the bench reads,
 // and the error plumbing of the C ABI (include/xsk_gpu.h).  Device code: xsk_echo_device.h.
 #include <errno.h>
 #include <stdlib.h>
@@ -70,7 +70,24 @@ const char* xsk_gpu_last_error(void) { return g_last_error; }
 
 size_t xsk_gpu_workspace_size(int device, uint32_t n) {
     if (device < 0) return 0;
-    return (size_t)echo_grid(n) * 4 * sizeof(unsigned long long);
+    // room for the partial rows of either launch geometry (round kernel: <= one workgroup per CU)
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    uint32_t g = echo_grid(n);
+    const uint32_t g6 = ntiles < kMaxCuBound ? ntiles : kMaxCuBound;
+    if (g6 > g) g = g6;
+    return (size_t)g * 4 * sizeof(unsigned long long);
+}
+
+// Compute units of `device` (cached): the round kernel launches one workgroup per CU.
+uint32_t xsk_gpu__num_cu(int device) {
+    static int cache[64];
+    if (device < 0 || device >= 64) return 0;
+    if (cache[device] <= 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) return 0;
+        cache[device] = v > (int)kMaxCuBound ? (int)kMaxCuBound : v;
+    }
+    return (uint32_t)cache[device];
 }
 
 
@@ -82,9 +99,13 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
         ((uintptr_t)d_recs & 15u))
         return -EINVAL;
     if (d_stats && !d_workspace) return -EINVAL;
+    if (umem_size >> 48) return -EINVAL;  // FrameMeta6 carries 48-bit UMEM offsets
     int device = 0;
     HIP_TRY(hipGetDevice(&device));
-    const uint32_t grid = echo_grid(n);
+    const uint32_t ncu = xsk_gpu__num_cu(device);
+    if (!ncu) return xsk_gpu__hip_fail(hipErrorInvalidDevice);
+    uint32_t grid = 0, tiles_per_wg = 0;
+    echo6_geometry(n, ncu, &grid, &tiles_per_wg);
     hipStream_t s = (hipStream_t)stream;
     EchoArgs args;
     args.umem = (uint8_t*)d_umem;
@@ -104,7 +125,7 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
         }
     }
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
-    echo_kernel5<kShipU, kShipMinW><<<dim3(grid), dim3(kThreads), 0, s>>>(args);
+    echo_kernel6<kShip6U, kShip6TPW><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     HIP_TRY(hipGetLastError());
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], s));
     if (d_stats) {

@@ -58,6 +58,7 @@ struct Counters {
 };
 
 // Counters: wave -> workgroup -> one partial row per workgroup (no atomics).
+template <int NW = kWaves>
 __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, unsigned long long (*s_cnt)[4],
                                                uint32_t wave, uint32_t lane) {
     if (!a.partials) return;
@@ -75,7 +76,7 @@ __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, un
     if (threadIdx.x < 4) {
         unsigned long long s = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) s += s_cnt[w][threadIdx.x];
+        for (int w = 0; w < NW; ++w) s += s_cnt[w][threadIdx.x];
         a.partials[blockIdx.x * 4 + threadIdx.x] = s;
     }
 }
@@ -197,10 +198,14 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
     }
 }
 
-// Header work of one frame (lane = frame) from its LDS row and its two folded row sums.
+// Header work of one frame (lane = frame) from its LDS row and its two folded row sums.  DEFER: the
+// verdict and record are returned in *verd_out / *rec_out instead of being stored (the round kernel
+// stores them in its write phase).
+template <bool DEFER = false>
 __device__ __forceinline__ bool header_phase5(const EchoArgs& a, uint8_t* row, uint32_t ip_raw, uint32_t ic_raw,
                                               uint64_t addr, uint32_t len, bool live, bool ok, bool parse,
-                                              uint32_t fi, Counters& cnt) {
+                                              uint32_t fi, Counters& cnt, u32x4* rec_out = nullptr,
+                                              uint32_t* verd_out = nullptr) {
     const uint32_t off = (uint32_t)addr & 15u;
     const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
     uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
@@ -282,9 +287,18 @@ __device__ __forceinline__ bool header_phase5(const EchoArgs& a, uint8_t* row, u
             }
         }
     }
+    if (DEFER) {
+        u32x4 r;
+        r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+        r.y = icode | (vihl << 8) | (eth_proto << 16);
+        r.z = (parse ? bswap16(csum_le) : 0u) | ((parse ? bswap16(csum_new_le) : 0u) << 16);
+        r.w = (parse ? ip_sum : 0u) | ((parse ? ic_sum : 0u) << 16);
+        *rec_out = r;
+        *verd_out = verdict;
+    }
     if (live) {
-        if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
-        if (a.recs) {
+        if (!DEFER && a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
+        if (!DEFER && a.recs) {
             u32x4 r;
             r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
             r.y = icode | (vihl << 8) | (eth_proto << 16);
@@ -463,15 +477,234 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel5(EchoArgs a) {
     store_partials(a, cnt, s_cnt, wave, lane);
 }
 
+
+// ================================================================================================
+// The round kernel (shipped).  Measured on cold 4 GiB slabs (tools/wexp.hip): a read stream that
+// meets scattered 64-B writes pays for them at DRAM read/write turnarounds (+61 us for 1 M header
+// sectors deferred to each tile's end, +69 us for the same bytes written to a contiguous side buffer)
+// while the same writes issued as a burst with no reads around them cost +20 us.  So the grid is
+// persistent -- one 16-wave workgroup per CU, every workgroup the same contiguous share of tiles --
+// and works in ROUNDS: each wave streams TPW tiles (the read phase: descriptors, payload, header
+// phase, patched windows into LDS, records into VGPRs), the workgroup meets at a barrier, and every
+// wave then stores its patched 64-B windows, records and verdicts (the write phase).  Equal shares
+// keep the workgroups' rounds in step, so the chip alternates between pure read and pure write
+// traffic instead of mixing them.
+// ================================================================================================
+constexpr int kWaves6 = 16;                 // waves per workgroup (one workgroup per CU)
+constexpr int kThreads6 = kWaves6 * 64;     // 1024
+constexpr int kShip6U = 4;                  // row-loads in flight per lane
+constexpr int kShip6TPW = 2;                // tiles per wave per round: 2048 frames per CU per round
+
+// 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
+struct FrameMeta6 {
+    uint32_t rel;     // a16 - window base (fast tiles); a16 >> 4 (short and far tiles)
+    uint32_t rowhi;   // frame end, row coordinates (0 unless parsed)
+    uint32_t lim;     // row bytes to load: max(rowhi, window bytes in the UMEM)
+    uint32_t packed;  // off | iphi << 8 | flags << 16 (1 ok, 2 parse) | (a16 >> 36) << 20
+};
+__device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
+    return ((uint64_t)(m.packed >> 20) << 36) | ((uint64_t)m.rel << 4);
+}
+
+template <int U, int TPW>
+__global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kWin];  // 128 KiB at TPW 2
+    __shared__ __attribute__((aligned(16))) FrameMeta6 s_meta[kWaves6][kTile];          // 16 KiB
+    __shared__ uint32_t s_sum[kWaves6][2][kTile];                                        // 8 KiB
+    __shared__ unsigned long long s_cnt[kWaves6][4];
+
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    FrameMeta6* meta = s_meta[wave];
+    uint32_t* sums_ic = s_sum[wave][0];
+    uint32_t* sums_ip = s_sum[wave][1];
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t_begin = blockIdx.x * tiles_per_wg;
+    const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+    constexpr uint32_t kRound = (uint32_t)kWaves6 * TPW;
+    Counters cnt;
+    uint32_t lane = threadIdx.x & 63u;
+
+    for (uint32_t r0 = t_begin; r0 < t_end; r0 += kRound) {  // workgroup-uniform
+        u32x4 rec[TPW];
+        uint32_t verd[TPW], alo[TPW], ahi[TPW];
+        uint64_t wbm[TPW];
+        // ================= read phase =================
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const uint32_t t = r0 + (uint32_t)i * kWaves6 + wave;
+            wbm[i] = 0ull;
+            rec[i] = u32x4{0u, 0u, 0u, 0u};
+            verd[i] = 0u;
+            alo[i] = 0u;
+            ahi[i] = 0u;
+            if (t >= t_end) continue;  // wave-uniform
+            asm volatile("" : "+v"(lane));
+            uint8_t* rows = s_hdr[wave][i];
+            const uint32_t q = lane >> 4, k = lane & 15u;
+            const uint32_t fi = t * kTile + lane;
+            // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
+            u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
+            if (fi < a.n) dsc = *(const u32x4*)(a.descs + fi);
+            const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
+            const uint32_t len = dsc.z;
+            const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+            const bool ok = fi < a.n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+            const bool parse = ok && len >= 20;
+            const uint64_t a16 = addr & ~15ull;
+            const uint32_t off = (uint32_t)addr & 15u;
+            const uint32_t rowhi = parse ? off + len : 0u;
+            const uint32_t win = parse ? (uint32_t)min(a.umem_size - a16, (uint64_t)kWin) : 0u;
+            const uint32_t lim = max(rowhi, win);
+            const uint32_t nit = (lim + 255u) >> 8;
+            const bool short_tile = __ballot(lim > (uint32_t)kWin) == 0ull;
+            uint64_t wlo = 0, span = ~0ull;
+            if (!short_tile) {
+                wlo = wave_min_u64(nit ? a16 : ~0ull);
+                span = wave_max_u64(nit ? a16 + lim : 0ull) - wlo;
+            }
+            const bool fast = !short_tile && span < 0x80000000ull;  // wave-uniform
+            {
+                FrameMeta6 m;
+                m.rel = fast ? (nit ? (uint32_t)(a16 - wlo) : 0u) : (uint32_t)(a16 >> 4);
+                m.rowhi = rowhi;
+                m.lim = lim;
+                m.packed = off | ((parse ? off + min(len, 34u) : 0u) << 8) | ((ok ? 1u : 0u) << 16) |
+                           ((parse ? 2u : 0u) << 16) | ((uint32_t)(a16 >> 36) << 20);
+                meta[lane] = m;
+            }
+            alo[i] = dsc.x;
+            ahi[i] = dsc.y;
+
+            // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
+            if (__ballot(nit != 0u) != 0ull) {
+                __builtin_amdgcn_wave_barrier();
+                WinLoader ld;
+                ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
+                                                         fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
+                if (short_tile) {
+                    // every frame within its 64-B window: 4 lanes per frame, 16 frames per wave-load
+                    const uint32_t kk = lane & 3u, ro = 16u * kk;
+                    u32x4 x[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const FrameMeta6& fm = meta[(uint32_t)r * 16u + (lane >> 2)];
+                        const bool in = ro < fm.lim;
+                        x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? meta6_a16(fm) + ro : 0ull)));
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                        const FrameMeta6& fm = meta[f];
+                        const uint32_t f_packed = fm.packed;
+                        const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                        *(u32x4*)(rows + f * kWin + ro) = v;
+                        const int f_off = (int)(f_packed & 0xFFu), f_iphi = (int)((f_packed >> 8) & 0xFFu);
+                        uint32_t rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
+                        uint32_t ric = fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
+                        rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);
+                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);
+                        rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0x4E, 0xF, 0xF, false);
+                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);
+                        if (kk == 0u) {
+                            sums_ic[f] = ric;
+                            sums_ip[f] = rip;
+                        }
+                    }
+                } else {
+                    for (uint32_t s = 0; s < 16; ++s) {
+                        const uint32_t f = 4u * s + q;
+                        const FrameMeta6& fm = meta[f];  // broadcast read: one entry per 16-lane row
+                        const uint32_t f_lim = fm.lim;
+                        const uint32_t f_nit = (f_lim + 255u) >> 8;
+                        const uint32_t ns = max(max(rdlane(f_nit, 0), rdlane(f_nit, 16)),
+                                                max(rdlane(f_nit, 32), rdlane(f_nit, 48)));
+                        if (ns == 0) continue;
+                        const uint32_t f_rowhi = fm.rowhi, f_packed = fm.packed;
+                        const uint32_t f_off = f_packed & 0xFFu, f_iphi = (f_packed >> 8) & 0xFFu;
+                        RowSums rs;
+                        if (fast) {
+                            ld.rel = fm.rel;
+                            stream_frame<U>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kWin, rs);
+                        } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
+                            FarLoader fl;
+                            fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
+                            stream_frame<U>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kWin, rs);
+                        }
+                        const uint32_t ric = row_sum_dpp(fold64(rs.ic));
+                        const uint32_t rip = row_sum_dpp(fold64(rs.ip));
+                        if (k == 15u) {
+                            sums_ic[f] = ric;
+                            sums_ip[f] = rip;
+                        }
+                    }
+                }
+            }
+
+            // ---- 3. header phase (lane = frame); the window stays patched in LDS ---------------------
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
+            const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
+            const bool wb = header_phase5<true>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, fi < a.n, ok,
+                                                parse, fi, cnt, &rec[i], &verd[i]);
+            wbm[i] = __ballot(wb);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();  // meta/sums are rewritten by the next tile
+        }
+
+        // ================= write phase: every wave of the workgroup has finished reading =================
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const uint32_t t = r0 + (uint32_t)i * kWaves6 + wave;
+            if (t >= t_end) continue;
+            const uint8_t* rows = s_hdr[wave][i];
+            if (wbm[i]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                    const uint32_t kk = lane & 3u;
+                    const uint32_t flo = (uint32_t)__shfl((int)alo[i], (int)f, 64);
+                    const uint32_t fhi = (uint32_t)__shfl((int)ahi[i], (int)f, 64);
+                    if ((wbm[i] >> f) & 1ull) {
+                        const uint64_t fa = (uint64_t)flo | ((uint64_t)fhi << 32);
+                        *(u32x4*)(a.umem + fa + 16u * kk) = *(const u32x4*)(rows + f * kWin + 16u * kk);
+                    }
+                }
+            }
+            const uint32_t fi = t * kTile + lane;
+            if (fi < a.n) {
+                if (a.recs) ((u32x4*)a.recs)[fi] = rec[i];
+                if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[i];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next round
+    }
+    store_partials<kWaves6>(a, cnt, s_cnt, wave, lane);
+}
+
 // Launch geometry: one workgroup per kWaves tiles (the dispatcher balances ragged tiles better than
 // a persistent grid: 315 vs 347 us at c3), capped so the partials workspace stays <= 512 KiB (the
 // kernel's tile loop covers larger batches).
 constexpr uint32_t kMaxGrid = 16384;
+constexpr uint32_t kMaxCuBound = 1024;  // workspace bound for the round kernel's one-workgroup-per-CU grid
 inline uint32_t echo_grid(uint32_t n) {
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     uint32_t g = (ntiles + kWaves - 1) / kWaves;
     if (g > kMaxGrid) g = kMaxGrid;
     return g < 1 ? 1 : g;
+}
+
+// Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
+inline void echo6_geometry(uint32_t n, uint32_t num_cu, uint32_t* grid, uint32_t* tiles_per_wg) {
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    uint32_t g = num_cu < 1 ? 1 : num_cu;
+    if (g > ntiles) g = ntiles < 1 ? 1 : ntiles;
+    const uint32_t per = (ntiles + g - 1) / g;
+    *tiles_per_wg = per < 1 ? 1 : per;
+    *grid = (ntiles + *tiles_per_wg - 1) / *tiles_per_wg;
+    if (*grid < 1) *grid = 1;
 }
 
 }  // namespace

@@ -320,8 +320,11 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
 
 extern "C" {
 
+uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip
+
 // Internal (not in include/xsk_gpu.h): kernel variants for the tuning sweep in tools/kbench.py.
 //   variant: 0 <P=4>, 1 <P=8>, 2 <P=2>, 3 <P=6>, 10+x = LITE (stream-only ceiling) of the same P
+//   50-54 = echo_kernel5 <U, min waves>, 60-64 = the round kernel echo_kernel6 <U, tiles per wave>
 //   max_grid: 0 = library default, else cap on workgroups
 int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t umem_size,
                           const struct xsk_gpu_desc* d_descs, uint32_t n, uint8_t* d_verdicts,
@@ -341,6 +344,23 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_workspace;
     hipStream_t s = (hipStream_t)stream;
+    if (variant >= 60 && variant < 70) {  // round kernel: max_grid = workgroups (0: one per CU)
+        int device = 0;
+        HIP_TRY(hipGetDevice(&device));
+        uint32_t g6 = 0, per = 0;
+        echo6_geometry(n, max_grid ? max_grid : xsk_gpu__num_cu(device), &g6, &per);
+        const dim3 gg(g6), bb(kThreads6);
+        switch (variant) {
+            case 60: echo_kernel6<4, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 61: echo_kernel6<6, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 62: echo_kernel6<8, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 63: echo_kernel6<4, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 64: echo_kernel6<2, 2><<<gg, bb, 0, s>>>(args, per); break;
+            default: return -EINVAL;
+        }
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
     const dim3 g(grid), b(kThreads);
     switch (variant) {
         case 0: echo_kernel<4, false><<<g, b, 0, s>>>(args); break;
