@@ -25,7 +25,8 @@ import torch  # noqa: E402
 
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-KERNEL = "echo_kernel5<4, 6>"  # the transform kernel xsk_gpu_echo_dev launches
+KERNEL = "echo_kernel6<4, 2>"  # the transform kernel xsk_gpu_echo_dev launches
+WIRE_KERNEL = "echo_wire_kernel<4>"  # xsk_gpu_echo_dev_opts with nonzero options (--opts)
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
@@ -176,6 +177,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--pool-cap", type=int, default=0, help="cap the batch pool (rehearsals on a shared GPU)")
+    ap.add_argument("--opts", type=int, default=0,
+                    help="wire-format options (XSK_GPU_OPT_*, xsk_gpu_echo_dev_opts); 0 = the reference's gates")
     args = ap.parse_args()
 
     import xsknet_amd as X
@@ -185,6 +188,9 @@ def main():
     rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", local)
     n, lo, hi, stride, seed, desc = CONFIGS[args.config]
+    kernel = KERNEL if args.opts == 0 else WIRE_KERNEL
+    if args.opts:
+        desc += f"; wire-format options {args.opts:#x} (xsk_gpu_echo_dev_opts)"
     K, W = args.steps, args.warmup
 
     # ---- batch pool: one fresh batch per step (generated on the GPU, bit-identical to the oracle) ----
@@ -221,7 +227,7 @@ def main():
         b = s % pool
         if rearm_in_loop and s >= pool:
             X.rearm_dev(umems[b], descss[b], verd, n, stream)  # conservative: counted inside the timing
-        X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream)
+        X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream, opts=args.opts)
 
     for s in range(W):
         step(s)
@@ -297,8 +303,8 @@ def main():
                        "rearm_in_timed_region": rearm_in_loop},
             "verified": bool(ok_all == world),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config, KERNEL),
-                         "kernel": KERNEL, "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config, kernel) if args.opts == 0 else None,
+                         "kernel": kernel, "kernel_avg_us": round(kern_avg_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": frame_bytes,
                          "read_ceiling_gbs": round(read_ceiling, 1)},
             "event_ms_per_step": round(ev_max / K, 4),

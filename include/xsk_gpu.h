@@ -74,14 +74,50 @@ enum xsk_gpu_verdict {
     XSK_GPU_DROP_NOT_IPV4 = 2,  /* bytes 12-13 != 08 00 (:135-138)                                  */
     XSK_GPU_DROP_NOT_ICMP = 3,  /* byte 23 != 1 (:140-143)                                          */
     XSK_GPU_DROP_NOT_ECHO = 4,  /* byte 34 != 8 (:144-147)                                          */
-    XSK_GPU_DROP_BAD_DESC = 5   /* build-added: the frame does not lie inside the UMEM, or
+    XSK_GPU_DROP_BAD_DESC = 5,  /* build-added: the frame does not lie inside the UMEM, or
                                    len > XSK_GPU_MAX_LEN (the reference would read out of bounds);
                                    never emitted for valid descriptors */
+    XSK_GPU_DROP_BAD_IP = 6,    /* wire mode, XSK_GPU_OPT_STRICT_IPV4 only: see below            */
+    XSK_GPU_DROP_BAD_CSUM = 7   /* wire mode, XSK_GPU_OPT_VERIFY_CSUM only: see below            */
 };
 
 /* Record flags (build-added verification of the INPUT frame; the reference never verifies). */
 #define XSK_GPU_F_IP_CSUM_OK 0x01u   /* len >= 34 and the IPv4 header [14,34) sums to 0xFFFF */
 #define XSK_GPU_F_ICMP_CSUM_OK 0x02u /* len >= 42 and the ICMP message [34,len) sums to 0xFFFF */
+#define XSK_GPU_F_VLAN 0x04u         /* wire mode: one or two VLAN tags were skipped           */
+#define XSK_GPU_F_IP_OPTIONS 0x08u   /* wire mode: IHL > 5 (IPv4 options present)             */
+
+/* ------------------------------------------------------------------------------------------ */
+/* Wire-format widening (build-added).  opts == 0 is the reference's gates */
+/* exactly (everything above).  Any nonzero opts selects "wire mode", which parses the headers  */
+/* instead of assuming the reference's fixed offsets (xsk_receive.c:120-121):                   */
+/*   l3 = 14; with XSK_GPU_OPT_VLAN up to two 802.1Q/802.1ad tags (TPID 0x8100 / 0x88A8) are     */
+/*        skipped, l3 += 4 each (a tag cut by the frame end: DROP_SHORT);                        */
+/*   DROP_SHORT if len < 14; DROP_NOT_IPV4 unless the (inner) ethertype is 0x0800;               */
+/*   DROP_SHORT if len < l3 + 20;                                                                */
+/*   with XSK_GPU_OPT_STRICT_IPV4: DROP_BAD_IP unless version == 4 and IHL >= 5, unless          */
+/*        IHL*4 + 8 <= tot_len and l3 + tot_len <= len, or if MF is set or the fragment offset is */
+/*        nonzero; the IPv4 header is IHL*4 bytes and the ICMP message is [l4, l3 + tot_len)     */
+/*        (Ethernet padding excluded); without it the header is 20 bytes and the message         */
+/*        [l4, len), l4 = l3 + header bytes;                                                     */
+/*   DROP_NOT_ICMP unless protocol (byte l3 + 9) == 1; DROP_SHORT if len < l4 + 8;               */
+/*   DROP_NOT_ECHO unless type (byte l4) == 8 (and, STRICT, code == 0);                          */
+/*   with XSK_GPU_OPT_VERIFY_CSUM: DROP_BAD_CSUM unless both the IPv4 header and the ICMP message */
+/*        sum to 0xFFFF;                                                                         */
+/*   otherwise TX_REPLY: process_packet's rewrite (xsk_receive.c:148-157) at the parsed offsets: */
+/*        MACs swapped, addresses at l3+12 / l3+16 swapped, type = 0, checksum at l4+2 updated   */
+/*        by csum_replace2(8 -> 0).                                                              */
+/* Wire-mode records: verdict always; every other field only once all three headers lie inside  */
+/* the frame (TX_REPLY, DROP_NOT_ECHO, DROP_BAD_CSUM), else zero: eth_proto = inner ethertype,   */
+/* ip_vihl / ip_proto / icmp_* from l3 / l4, ip_sum over [l3, l4), icmp_sum over the message,    */
+/* flags IP_CSUM_OK / ICMP_CSUM_OK (sum == 0xFFFF), VLAN, IP_OPTIONS.  Wire mode reads only      */
+/* [addr, addr + len) plus the 16-B-aligned 128-byte header window (within the UMEM), and a      */
+/* descriptor whose [addr, addr + len) leaves the UMEM is DROP_BAD_DESC.                         */
+/* ------------------------------------------------------------------------------------------ */
+#define XSK_GPU_OPT_STRICT_IPV4 0x1u
+#define XSK_GPU_OPT_VLAN 0x2u
+#define XSK_GPU_OPT_VERIFY_CSUM 0x4u
+#define XSK_GPU_OPT_ALL 0x7u
 
 /* Optional 16-byte per-frame result record. Parsed fields are those the reference reads
  * (xsk_receive.c:135,140,144,157); they are all zero when len < 20 because the reference reads
@@ -123,6 +159,12 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                      void* d_workspace, void* stream);
 
+/* xsk_gpu_echo_dev() with wire-format options (XSK_GPU_OPT_*; 0 = xsk_gpu_echo_dev() exactly).
+ * Unknown option bits are -EINVAL. */
+int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                          uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
+                          struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Host-UMEM entry points: the drop-in for the client's RX loop (xsk_receive.c:192-237).       */
 /* ------------------------------------------------------------------------------------------ */
@@ -148,6 +190,10 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
  * xsk_gpu_echo_dev(); `verdicts`, `recs` and `stats` are host pointers (each may be NULL). */
 int xsk_gpu_process(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                     struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+
+/* Wire-format options (XSK_GPU_OPT_*) for this context's later xsk_gpu_process() / xsk_gpu_rx_step()
+ * calls (0 at init: the reference's gates). */
+int xsk_gpu_set_options(xsk_gpu_ctx* ctx, uint32_t opts);
 
 /* Release device buffers and unregister the UMEM. NULL is a no-op. */
 void xsk_gpu_fini(xsk_gpu_ctx* ctx);

@@ -321,6 +321,114 @@ void oracle_rearm(uint8_t* umem, const struct xsk_gpu_desc* descs, const uint8_t
 }
 
 /* ---------------------------------------------------------------------------------------------- */
+/* Wire-format widening (build-added, the reference has no such mode).        */
+/* The spec is include/xsk_gpu.h (XSK_GPU_OPT_*); the rewrite itself is process_packet's           */
+/* (xsk_receive.c:148-157) at the parsed offsets.                                                   */
+/* ---------------------------------------------------------------------------------------------- */
+
+/* One frame in wire mode.  Returns the verdict; fills *r (zeroed first) and rewrites TX_REPLY frames. */
+static int wire_one(uint8_t* p, uint32_t len, uint32_t opts, struct xsk_gpu_rec* r) {
+    memset(r, 0, sizeof *r);
+    if (len < 14) return XSK_GPU_DROP_SHORT;
+    uint32_t l3 = 14;
+    uint16_t et = ld_be16(p + 12);
+    int tags = 0;
+    if (opts & XSK_GPU_OPT_VLAN) {
+        while (tags < 2 && (et == 0x8100 || et == 0x88A8)) { /* 802.1Q / 802.1ad tag: TPID, TCI */
+            if (len < l3 + 4) return XSK_GPU_DROP_SHORT;
+            et = ld_be16(p + l3 + 2);
+            l3 += 4;
+            tags++;
+        }
+    }
+    if (et != 0x0800) return XSK_GPU_DROP_NOT_IPV4;
+    if (len < l3 + 20) return XSK_GPU_DROP_SHORT;
+    uint32_t hl = 20, end = len;
+    if (opts & XSK_GPU_OPT_STRICT_IPV4) {
+        const uint8_t vihl = p[l3];
+        if ((vihl >> 4) != 4 || (vihl & 15) < 5) return XSK_GPU_DROP_BAD_IP;
+        hl = 4u * (vihl & 15u);
+        const uint32_t tot = ld_be16(p + l3 + 2);
+        if (tot < hl + 8 || l3 + tot > len) return XSK_GPU_DROP_BAD_IP; /* also covers len < l3 + hl + 8 */
+        if (ld_be16(p + l3 + 6) & 0x3FFF) return XSK_GPU_DROP_BAD_IP;  /* MF set or fragment offset != 0 */
+        end = l3 + tot;                                                 /* Ethernet padding excluded */
+    }
+    if (p[l3 + 9] != 1) return XSK_GPU_DROP_NOT_ICMP;
+    const uint32_t l4 = l3 + hl;
+    if (len < l4 + 8) return XSK_GPU_DROP_SHORT;
+    /* every header lies inside the frame from here on: the record is filled */
+    r->eth_proto = et;
+    r->ip_vihl = p[l3];
+    r->ip_proto = p[l3 + 9];
+    r->icmp_type = p[l4];
+    r->icmp_code = p[l4 + 1];
+    r->icmp_csum_in = ld_be16(p + l4 + 2);
+    r->ip_sum = oracle_fold_sum(p, l3, l3 + hl);
+    r->icmp_sum = oracle_fold_sum(p, l4, end);
+    if (r->ip_sum == 0xFFFF) r->flags |= XSK_GPU_F_IP_CSUM_OK;
+    if (r->icmp_sum == 0xFFFF) r->flags |= XSK_GPU_F_ICMP_CSUM_OK;
+    if (tags) r->flags |= XSK_GPU_F_VLAN;
+    if (hl > 20) r->flags |= XSK_GPU_F_IP_OPTIONS;
+    int v;
+    if (p[l4] != 8 || ((opts & XSK_GPU_OPT_STRICT_IPV4) && p[l4 + 1] != 0)) v = XSK_GPU_DROP_NOT_ECHO;
+    else if ((opts & XSK_GPU_OPT_VERIFY_CSUM) && (r->ip_sum != 0xFFFF || r->icmp_sum != 0xFFFF)) v = XSK_GPU_DROP_BAD_CSUM;
+    else v = XSK_GPU_TX_REPLY;
+    if (v == XSK_GPU_TX_REPLY) { /* xsk_receive.c:148-157 at the parsed offsets */
+        uint8_t tmp[6];
+        memcpy(tmp, p, 6);
+        memcpy(p, p + 6, 6);
+        memcpy(p + 6, tmp, 6);
+        uint8_t ip[4];
+        memcpy(ip, p + l3 + 12, 4);
+        memcpy(p + l3 + 12, p + l3 + 16, 4);
+        memcpy(p + l3 + 16, ip, 4);
+        p[l4] = 0;
+        uint16_t c = ld_le16(p + l4 + 2);
+        oracle_csum_replace2(&c, 8, 0);
+        st_le16(p + l4 + 2, c);
+    }
+    r->verdict = (uint8_t)v;
+    r->icmp_csum_out = ld_be16(p + l4 + 2);
+    return v;
+}
+
+void oracle_echo_batch_opts(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
+                            uint32_t opts, uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats) {
+    if (opts == 0) {
+        oracle_echo_batch(umem, umem_size, descs, n, verdicts, recs, stats);
+        return;
+    }
+    uint64_t rxb = 0, txp = 0, txb = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t a = descs[i].addr;
+        const uint32_t len = descs[i].len;
+        struct xsk_gpu_rec r;
+        int v;
+        if (len > XSK_GPU_MAX_LEN || a > umem_size || len > umem_size - a) { /* wire mode reads [addr, addr+len) */
+            memset(&r, 0, sizeof r);
+            v = XSK_GPU_DROP_BAD_DESC;
+            r.verdict = (uint8_t)v;
+        } else {
+            v = wire_one(umem + a, len, opts, &r);
+            r.verdict = (uint8_t)v;
+        }
+        if (recs) recs[i] = r;
+        if (verdicts) verdicts[i] = (uint8_t)v;
+        if (v == XSK_GPU_TX_REPLY) {
+            txp++;
+            txb += len;
+        }
+        rxb += len;
+    }
+    if (stats) {
+        stats->rx_packets += n;
+        stats->rx_bytes += rxb;
+        stats->tx_packets += txp;
+        stats->tx_bytes += txb;
+    }
+}
+
+/* ---------------------------------------------------------------------------------------------- */
 /* XDP ingress filter (src/kern/inner_xdp.c:26-61; phy_xdp.c:39-81 applies the same tests)         */
 /* ---------------------------------------------------------------------------------------------- */
 

@@ -40,6 +40,11 @@ void oracle_echo_batch(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_d
 void oracle_echo_batch_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
                           uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats, int threads);
 
+/* Full contract of xsk_gpu_echo_dev_opts(): opts == 0 is oracle_echo_batch(); otherwise the wire-format
+ * widening of include/xsk_gpu.h (XSK_GPU_OPT_*), build-added. */
+void oracle_echo_batch_opts(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
+                            uint32_t opts, uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+
 /* Reference-equivalent work only (gates + rewrite + counters; no full-payload sums, no records):
  * the CPU-baseline variant that does exactly what process_packet does. */
 void oracle_echo_batch_hdr(uint8_t* umem, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,

@@ -180,3 +180,72 @@ def test_xdp_classify_batch_compacts_in_order():
     v, _, _ = oracle.echo_batch(umem.copy(), descs)
     assert (act[(v == 0) & (descs["len"] >= 34)] == 4).all()
     assert (act[(v == 0) & (descs["len"] < 34)] == 1).all()
+
+
+# ---- wire-format widening (xsk_gpu_echo_dev_opts) -------------------------------
+def _wire_golden():
+    import json
+    import os
+    from tests.conftest import ROOT
+    with open(os.path.join(ROOT, "tests", "golden", "wire.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("off", [0, 1, 3, 16])
+def test_wire_oracle_matches_golden(off):
+    """The C oracle's wire mode against the independent Python restatement's vectors (all 7 option sets)."""
+    for case in _wire_golden():
+        fr = bytes.fromhex(case["frame"])
+        L = case["len"]
+        for opts, exp in case["results"].items():
+            umem = np.zeros(2048, np.uint8)
+            umem[off:off + len(fr)] = np.frombuffer(fr, np.uint8)
+            d = np.zeros(1, oracle.DESC_DTYPE)
+            d[0] = (off, L, 0)
+            v, r, s = oracle.echo_batch_opts(umem, d, int(opts))
+            assert v[0] == exp["verdict"], (case["name"], L, opts)
+            assert {k: int(r[0][k]) for k in r.dtype.names} == exp["rec"], (case["name"], L, opts)
+            assert umem[off:off + max(L, 1)].tobytes().hex() == exp["out"], (case["name"], L, opts)
+            assert int(s["tx_packets"]) == (1 if exp["verdict"] == 0 else 0)
+
+
+def test_wire_opts_zero_is_reference_mode():
+    umem = np.zeros(300 * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, 300, 0, 2048, seed=0x5EED0B0B, mode=1, len_lo=20, len_hi=1500)
+    a, b = umem.copy(), umem.copy()
+    va, ra, sa = oracle.echo_batch(a, descs)
+    vb, rb, sb = oracle.echo_batch_opts(b, descs, 0)
+    assert (va == vb).all() and (ra == rb).all() and (a == b).all() and sa == sb
+
+
+@pytest.mark.parametrize("opts", [1, 2, 3, 4, 5, 6, 7])
+def test_wire_oracle_matches_python_spec_on_random_traffic(opts):
+    """Two independent restatements of the wire spec agree on random mixed traffic."""
+    from tests.wire_frames import G, mixed_batch
+    umem, descs = mixed_batch(600, 2048, seed=opts, offsets=True)
+    work = umem.copy()
+    v, r, s = oracle.echo_batch_opts(work, descs, opts)
+    tx = 0
+    for i, d in enumerate(descs):
+        a, L = int(d["addr"]), int(d["len"])
+        frame = umem[a:a + 128 + L].tobytes()
+        ev, erec, eout = G.expect(frame, L, opts)
+        assert v[i] == ev, (i, opts)
+        assert {k: int(r[i][k]) for k in r.dtype.names} == erec, (i, opts)
+        assert work[a:a + L].tobytes() == eout[:L], (i, opts)
+        tx += ev == 0
+    assert int(s["tx_packets"]) == tx and int(s["rx_packets"]) == len(descs)
+    # every reply of a verified request verifies again (the incremental update is exact)
+    if opts & 4:
+        for i in np.nonzero(v == 0)[0]:
+            a = int(descs[i]["addr"])
+            hl = 4 * (int(r[i]["ip_vihl"]) & 15) if opts & 1 else 20
+            frame = work[a:a + int(descs[i]["len"])].tobytes()
+            # locate l3 by skipping tags exactly like the spec
+            l3, et = 14, (frame[12] << 8) | frame[13]
+            while opts & 2 and l3 < 22 and et in (0x8100, 0x88A8):
+                et = (frame[l3 + 2] << 8) | frame[l3 + 3]
+                l3 += 4
+            l4 = l3 + hl
+            end = l3 + ((frame[l3 + 2] << 8) | frame[l3 + 3]) if opts & 1 else len(frame)
+            assert G.csum16(frame[l4:end]) == 0xFFFF

@@ -30,6 +30,8 @@ LAYOUTS = {
     "c3_s1504": (1 << 20, 1500, 1500, 1504),
     "c2_s64": (1 << 20, 64, 64, 64),
     "c4_s2048": (1 << 20, 64, 1500, 2048),
+    "p98_s2048": (1 << 20, 98, 98, 2048),      # a default ping (56-B payload) per frame
+    "m512_s2048": (1 << 20, 64, 512, 2048),
 }
 
 

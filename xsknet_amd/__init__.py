@@ -23,14 +23,20 @@ __all__ = [
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
     "MODE_ZEROCOPY", "MODE_STAGED", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
-    "classify_dev", "XDP_DROP", "XDP_PASS", "XDP_REDIRECT",
+    "classify_dev", "XDP_DROP", "XDP_PASS", "XDP_REDIRECT", "DROP_BAD_IP", "DROP_BAD_CSUM",
+    "OPT_STRICT_IPV4", "OPT_VLAN", "OPT_VERIFY_CSUM", "OPT_ALL", "F_IP_CSUM_OK", "F_ICMP_CSUM_OK", "F_VLAN",
+    "F_IP_OPTIONS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxsknet_amd.so")
 
-TX_REPLY, DROP_SHORT, DROP_NOT_IPV4, DROP_NOT_ICMP, DROP_NOT_ECHO, DROP_BAD_DESC = range(6)
-VERDICTS = ["TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC"]
+TX_REPLY, DROP_SHORT, DROP_NOT_IPV4, DROP_NOT_ICMP, DROP_NOT_ECHO, DROP_BAD_DESC, DROP_BAD_IP, DROP_BAD_CSUM = range(8)
+VERDICTS = ["TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
+            "DROP_BAD_IP", "DROP_BAD_CSUM"]
+# wire-format options (include/xsk_gpu.h XSK_GPU_OPT_*) and record flags
+OPT_STRICT_IPV4, OPT_VLAN, OPT_VERIFY_CSUM, OPT_ALL = 1, 2, 4, 7
+F_IP_CSUM_OK, F_ICMP_CSUM_OK, F_VLAN, F_IP_OPTIONS = 1, 2, 4, 8
 MODE_ZEROCOPY, MODE_STAGED = 0, 1
 
 # struct xsk_gpu_desc == struct xdp_desc (linux/if_xdp.h)
@@ -84,6 +90,8 @@ _SIGS = {
     "xsk_gpu_last_error": ([], C.c_char_p),
     "xsk_gpu_workspace_size": ([C.c_int, C.c_uint32], C.c_size_t),
     "xsk_gpu_echo_dev": ([_P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu_echo_dev_opts": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu_set_options": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu_init": ([C.POINTER(_P), C.c_int, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
     "xsk_gpu_process": ([_P, _P, C.c_uint32, _P, _P, _P], C.c_int),
     "xsk_gpu_fini": ([_P], None),
@@ -139,8 +147,15 @@ def workspace_size(device: int, n: int) -> int:
     return int(lib().xsk_gpu_workspace_size(device, n))
 
 
-def echo_dev(umem, descs, n: int, verdicts=None, recs=None, stats=None, workspace=None, stream=None) -> None:
-    """xsk_gpu_echo_dev on torch device tensors (uint8 umem, uint8/int64 views of the structs)."""
+def echo_dev(umem, descs, n: int, verdicts=None, recs=None, stats=None, workspace=None, stream=None,
+             opts: int = 0) -> None:
+    """xsk_gpu_echo_dev (opts == 0) / xsk_gpu_echo_dev_opts on torch device tensors (uint8 umem,
+    uint8/int64 views of the structs)."""
+    if opts:
+        _check("xsk_gpu_echo_dev_opts", lib().xsk_gpu_echo_dev_opts(
+            _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, opts, _ptr(verdicts), _ptr(recs),
+            _ptr(stats), _ptr(workspace), _stream_ptr(stream)))
+        return
     _check("xsk_gpu_echo_dev", lib().xsk_gpu_echo_dev(
         _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, _ptr(verdicts), _ptr(recs), _ptr(stats),
         _ptr(workspace), _stream_ptr(stream)))
@@ -191,12 +206,18 @@ def timing_read():
 class EchoContext:
     """Host-UMEM drop-in (xsk_gpu_init / xsk_gpu_process / xsk_gpu_fini) over a numpy uint8 UMEM."""
 
-    def __init__(self, umem: np.ndarray, device: int = 0, max_batch: int = 4096, mode: int = MODE_ZEROCOPY):
+    def __init__(self, umem: np.ndarray, device: int = 0, max_batch: int = 4096, mode: int = MODE_ZEROCOPY,
+                 opts: int = 0):
         assert umem.dtype == np.uint8 and umem.flags.c_contiguous
         self.umem = umem
         self._ctx = C.c_void_p()
         _check("xsk_gpu_init", lib().xsk_gpu_init(C.byref(self._ctx), device, umem.ctypes.data, umem.nbytes,
                                                   max_batch, mode))
+        if opts:
+            self.set_options(opts)
+
+    def set_options(self, opts: int) -> None:
+        _check("xsk_gpu_set_options", lib().xsk_gpu_set_options(self._ctx, opts))
 
     def process(self, descs: np.ndarray, want_recs: bool = True):
         n = len(descs)

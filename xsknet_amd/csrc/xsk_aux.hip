@@ -117,15 +117,19 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthArgs a) {
     }
 }
 
-// Staged host mode: gather the 38 rewritten header bytes of every TX_REPLY frame into a packed
-// [n][48] array so the host can scatter them back into its UMEM (never touching unowned bytes).
+// Staged host mode: gather the rewritten header bytes of every TX_REPLY frame into a packed [n][96]
+// array so the host can scatter them back into its UMEM (never touching unowned bytes): bytes [0, 38)
+// in reference mode, [0, min(len, 96)) in wire mode (its rewrite ends at l4 + 4 <= 86 <= len).
+constexpr uint32_t kPack = 96;
 __global__ __launch_bounds__(256) void pack_headers_kernel(const uint8_t* umem, const xsk_gpu_desc* descs,
-                                                           const uint8_t* verdicts, uint32_t n, uint8_t* pack) {
+                                                           const uint8_t* verdicts, uint32_t n, uint8_t* pack,
+                                                           uint32_t wire) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n || verdicts[i] != XSK_GPU_TX_REPLY) return;
     const uint8_t* p = umem + descs[i].addr;
-    uint8_t* q = pack + (uint64_t)i * 48u;
-    for (int k = 0; k < 38; ++k) q[k] = p[k];
+    uint8_t* q = pack + (uint64_t)i * kPack;
+    const uint32_t w = wire ? min(descs[i].len, kPack) : 38u;
+    for (uint32_t k = 0; k < w; ++k) q[k] = p[k];
 }
 
 // Re-arm TX_REPLY frames (lane per frame, byte granular: bench utility, not the hot path).
@@ -220,10 +224,10 @@ int xsk_gpu_rearm_dev(void* d_umem, const struct xsk_gpu_desc* d_descs, const ui
 }
 
 int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
-                              uint32_t n, uint8_t* d_pack, void* stream) {
+                              uint32_t n, uint8_t* d_pack, uint32_t wire, void* stream) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(pack_headers_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                       (const uint8_t*)d_umem, d_descs, d_verdicts, n, d_pack);
+                       (const uint8_t*)d_umem, d_descs, d_verdicts, n, d_pack, wire);
     HIP_TRY(hipGetLastError());
     return 0;
 }

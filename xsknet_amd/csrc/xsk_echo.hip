@@ -53,6 +53,15 @@ struct Timer {
 Timer g_timer;
 std::mutex g_timer_mu;
 
+// Timer slot for the next transform launch (-1 when timing is off or full).
+int timer_slot(int device) {
+    std::lock_guard<std::mutex> lk(g_timer_mu);
+    if (!g_timer.on || g_timer.count >= kTimerCap) return -1;
+    const int slot = g_timer.count++;
+    g_timer.dev[slot] = device;
+    return slot;
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -116,14 +125,7 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
     args.recs = d_recs;
     args.partials = d_stats ? (unsigned long long*)d_workspace : nullptr;
 
-    int slot = -1;
-    {
-        std::lock_guard<std::mutex> lk(g_timer_mu);
-        if (g_timer.on && g_timer.count < kTimerCap) {
-            slot = g_timer.count++;
-            g_timer.dev[slot] = device;
-        }
-    }
+    const int slot = timer_slot(device);
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
     echo_kernel6<kShip6U, kShip6TPW><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     HIP_TRY(hipGetLastError());
@@ -131,6 +133,38 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
     if (d_stats) {
         hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, s, (const unsigned long long*)d_workspace, grid,
                            d_stats);
+        HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, void* d_partials,
+                           uint32_t* grid_out, void* stream);  // xsk_wire.hip
+
+int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                          uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
+                          struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream) {
+    if (opts & ~XSK_GPU_OPT_ALL) return -EINVAL;
+    if (opts == 0)
+        return xsk_gpu_echo_dev(d_umem, umem_size, d_descs, n, d_verdicts, d_recs, d_stats, d_workspace, stream);
+    if (n == 0) return 0;
+    if (!d_umem || !d_descs || ((uintptr_t)d_umem & 15u) || (umem_size & 15u) || ((uintptr_t)d_descs & 15u) ||
+        ((uintptr_t)d_recs & 15u))
+        return -EINVAL;
+    if (d_stats && !d_workspace) return -EINVAL;
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    uint32_t grid = 0;
+    const int slot = timer_slot(device);
+    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], (hipStream_t)stream));
+    const int rc = xsk_gpu__echo_wire_dev(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs,
+                                          d_stats ? d_workspace : nullptr, &grid, stream);
+    if (rc) return rc;
+    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], (hipStream_t)stream));
+    if (d_stats) {
+        hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
+                           (const unsigned long long*)d_workspace, grid, d_stats);
         HIP_TRY(hipGetLastError());
     }
     return 0;

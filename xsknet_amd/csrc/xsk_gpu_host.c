@@ -27,14 +27,17 @@
 #include "../../include/xsk_gpu.h"
 
 int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
-                              uint32_t n, uint8_t* d_pack, void* stream);
+                              uint32_t n, uint8_t* d_pack, uint32_t wire, void* stream);
 
 #define NSTREAMS 2
 #define CHUNK_FRAMES 32768u /* staged pipeline granule: ~49 MB of 1500-B frames per copy-in */
+#define PACK 96u            /* staged: bytes per frame of the packed rewritten headers (wire mode <= 86) */
+#define WIRE_WIN 128u       /* wire mode's header window (xsk_wire.hip) */
 
 struct xsk_gpu_ctx {
     int device;
     int mode;
+    uint32_t opts;  /* XSK_GPU_OPT_* for xsk_gpu_echo_dev_opts() */
     uint8_t* umem;
     uint64_t umem_size;
     uint32_t max_batch;
@@ -45,7 +48,7 @@ struct xsk_gpu_ctx {
     struct xsk_gpu_rec* d_recs;
     struct xsk_gpu_stats* d_stats; /* [max_chunks] */
     void* d_ws[NSTREAMS];
-    uint8_t* d_pack;  /* STAGED: [max_batch][48] rewritten headers */
+    uint8_t* d_pack;  /* STAGED: [max_batch][PACK] rewritten headers */
     uint8_t* h_pack;  /* STAGED: pinned host copy of d_pack */
     uint8_t* h_verd;  /* pinned verdict staging */
     struct xsk_gpu_stats* h_stats; /* [max_chunks] */
@@ -114,8 +117,8 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
         TRY(hipHostGetDevicePointer((void**)&c->d_umem, umem, 0));
     } else {
         TRY(hipMalloc((void**)&c->d_umem, umem_size));
-        TRY(hipMalloc((void**)&c->d_pack, (size_t)max_batch * 48u));
-        TRY(hipHostMalloc((void**)&c->h_pack, (size_t)max_batch * 48u, hipHostMallocDefault));
+        TRY(hipMalloc((void**)&c->d_pack, (size_t)max_batch * PACK));
+        TRY(hipHostMalloc((void**)&c->h_pack, (size_t)max_batch * PACK, hipHostMallocDefault));
     }
     TRY(hipMalloc((void**)&c->d_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc)));
     TRY(hipMalloc((void**)&c->d_verdicts, max_batch));
@@ -156,16 +159,23 @@ static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
     return s;
 }
 
-/* Copy-in of the bytes the kernel may read for frames d[0..n): [align16(addr), align16(addr)+64) u
- * [addr, addr+len), clipped to the UMEM. */
+int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
+    if (!c || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
+    c->opts = opts;
+    return 0;
+}
+
+/* Copy-in of the bytes the kernel may read for frames d[0..n): [align16(addr), align16(addr)+W) u
+ * [addr, addr+len), clipped to the UMEM; W = 64 (128 in wire mode). */
 static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n, hipStream_t st) {
     uint64_t lo = UINT64_MAX, hi = 0, width = 0;
+    const uint64_t win = c->opts ? WIRE_WIN : 64u;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t a = d[i].addr;
         if (a >= c->umem_size) continue; /* BAD_DESC: the kernel reads nothing */
         const uint64_t a16 = a & ~15ull;
         uint64_t e = a + (d[i].len > 48 ? d[i].len : 48);
-        if (e < a16 + 64) e = a16 + 64;
+        if (e < a16 + win) e = a16 + win;
         e = (e + 15) & ~15ull;
         if (e > c->umem_size) e = c->umem_size;
         if (a16 < lo) lo = a16;
@@ -197,13 +207,14 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
         rc = stage_in(c, descs + i0, n, st);
         if (rc) goto out;
     }
-    rc = xsk_gpu_echo_dev(c->d_umem, c->umem_size, dd, n, c->d_verdicts + i0, want_recs ? c->d_recs + i0 : NULL,
-                          c->d_stats + ci, c->d_ws[s], st);
+    rc = xsk_gpu_echo_dev_opts(c->d_umem, c->umem_size, dd, n, c->opts, c->d_verdicts + i0,
+                               want_recs ? c->d_recs + i0 : NULL, c->d_stats + ci, c->d_ws[s], st);
     if (rc) goto out;
     if (c->mode == XSK_GPU_MODE_STAGED) {
-        rc = xsk_gpu__pack_headers_dev(c->d_umem, dd, c->d_verdicts + i0, n, c->d_pack + (size_t)i0 * 48u, st);
+        rc = xsk_gpu__pack_headers_dev(c->d_umem, dd, c->d_verdicts + i0, n, c->d_pack + (size_t)i0 * PACK,
+                                       c->opts != 0, st);
         if (rc) goto out;
-        TRY(hipMemcpyAsync(c->h_pack + (size_t)i0 * 48u, c->d_pack + (size_t)i0 * 48u, (size_t)n * 48u,
+        TRY(hipMemcpyAsync(c->h_pack + (size_t)i0 * PACK, c->d_pack + (size_t)i0 * PACK, (size_t)n * PACK,
                            hipMemcpyDeviceToHost, st));
     }
     TRY(hipMemcpyAsync(c->h_verd + i0, c->d_verdicts + i0, n, hipMemcpyDeviceToHost, st));
@@ -234,8 +245,12 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
             goto drain;
         }
         if (c->mode == XSK_GPU_MODE_STAGED) { /* scatter the rewritten bytes of this chunk's replies */
-            for (uint32_t i = i0; i < i0 + m; i++)
-                if (c->h_verd[i] == XSK_GPU_TX_REPLY) memcpy(c->umem + descs[i].addr, c->h_pack + (size_t)i * 48u, 38);
+            for (uint32_t i = i0; i < i0 + m; i++) {
+                if (c->h_verd[i] != XSK_GPU_TX_REPLY) continue;
+                /* reference mode rewrites bytes [0, 38); wire mode bytes below l4 + 4 <= 86 <= len */
+                const uint32_t w = c->opts ? (descs[i].len < PACK ? descs[i].len : PACK) : 38u;
+                memcpy(c->umem + descs[i].addr, c->h_pack + (size_t)i * PACK, w);
+            }
         }
         if (stats) {
             stats->rx_packets += c->h_stats[ci].rx_packets;

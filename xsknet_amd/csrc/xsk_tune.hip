@@ -356,6 +356,11 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 62: echo_kernel6<8, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 63: echo_kernel6<4, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 64: echo_kernel6<2, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 65: echo_kernel7<4, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 66: echo_kernel7<6, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 67: echo_kernel7<3, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 68: echo_kernel7<4, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 69: echo_kernel7<2, 2><<<gg, bb, 0, s>>>(args, per); break;
             default: return -EINVAL;
         }
         HIP_TRY(hipGetLastError());
