@@ -502,6 +502,7 @@ constexpr int kWaves6 = 16;                 // waves per workgroup (one workgrou
 constexpr int kThreads6 = kWaves6 * 64;     // 1024
 constexpr int kShip6U = 4;                  // row-loads in flight per lane
 constexpr int kShip6TPW = 2;                // tiles per wave per round: 2048 frames per CU per round
+constexpr int kShip6Sync = 2;               // heavy waves wait for the round, light ones go ahead
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -514,12 +515,23 @@ __device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
     return ((uint64_t)(m.packed >> 20) << 36) | ((uint64_t)m.rel << 4);
 }
 
-template <int U, int TPW>
+// SYNC: how a wave enters its write phase.  0: at once; 1: workgroup barrier (all waves read, then
+// all write); 2: a wave whose tiles averaged >= kHeavyLen bytes per frame waits until every wave of
+// the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
+// phase separation pays where reads dominate, and costs latency hiding where frames are short.
+constexpr uint32_t kHeavyLen = 1024;
+template <int U, int TPW, int SYNC = 1>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kWin];  // 128 KiB at TPW 2
     __shared__ __attribute__((aligned(16))) FrameMeta6 s_meta[kWaves6][kTile];          // 16 KiB
     __shared__ uint32_t s_sum[kWaves6][2][kTile];                                        // 8 KiB
     __shared__ unsigned long long s_cnt[kWaves6][4];
+    __shared__ uint32_t s_arrive;
+    if (SYNC == 2) {
+        if (threadIdx.x == 0) s_arrive = 0u;
+        __syncthreads();
+    }
+    uint32_t rounds_done = 0;
 
     const uint32_t wave = uniform(threadIdx.x >> 6);
     FrameMeta6* meta = s_meta[wave];
@@ -536,6 +548,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         u32x4 rec[TPW];
         uint32_t verd[TPW], alo[TPW], ahi[TPW];
         uint64_t wbm[TPW];
+        uint32_t round_bytes = 0;  // SYNC 2: frame bytes this wave read this round (wave-uniform)
         // ================= read phase =================
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
@@ -582,6 +595,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             }
             alo[i] = dsc.x;
             ahi[i] = dsc.y;
+            if (SYNC == 2) round_bytes += wave_sum_u32(fi < a.n ? min(len, 65536u) : 0u);
 
             // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
             if (__ballot(nit != 0u) != 0ull) {
@@ -661,7 +675,16 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         }
 
         // ================= write phase: every wave of the workgroup has finished reading =================
-        __syncthreads();
+        if (SYNC == 1) __syncthreads();
+        if (SYNC == 2) {
+            ++rounds_done;
+            if (lane == 0) atomicAdd(&s_arrive, 1u);
+            if (uniform(round_bytes) >= kHeavyLen * kTile * TPW) {
+                while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                       rounds_done * (uint32_t)kWaves6)
+                    __builtin_amdgcn_s_sleep(2);
+            }
+        }
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const uint32_t t = r0 + (uint32_t)i * kWaves6 + wave;

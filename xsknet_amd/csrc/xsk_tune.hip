@@ -344,7 +344,7 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_workspace;
     hipStream_t s = (hipStream_t)stream;
-    if (variant >= 60 && variant < 70) {  // round kernel: max_grid = workgroups (0: one per CU)
+    if (variant >= 60 && variant < 80) {  // round kernel: max_grid = workgroups (0: one per CU)
         int device = 0;
         HIP_TRY(hipGetDevice(&device));
         uint32_t g6 = 0, per = 0;
@@ -361,6 +361,9 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 67: echo_kernel7<3, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 68: echo_kernel7<4, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 69: echo_kernel7<2, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 70: echo_kernel6<4, 2, 0><<<gg, bb, 0, s>>>(args, per); break;
+            case 71: echo_kernel6<4, 1, 0><<<gg, bb, 0, s>>>(args, per); break;
+            case 72: echo_kernel6<4, 2, 2><<<gg, bb, 0, s>>>(args, per); break;
             default: return -EINVAL;
         }
         HIP_TRY(hipGetLastError());
