@@ -81,6 +81,12 @@ __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, un
     }
 }
 
+__device__ __forceinline__ uint32_t max_nit_lane(uint32_t x) {  // wave max (every lane gets it)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return x;
+}
+
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {  // uniform result (SGPRs)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -503,6 +509,7 @@ constexpr int kThreads6 = kWaves6 * 64;     // 1024
 constexpr int kShip6U = 4;                  // row-loads in flight per lane
 constexpr int kShip6TPW = 2;                // tiles per wave per round: 2048 frames per CU per round
 constexpr int kShip6Sync = 2;               // heavy waves wait for the round, light ones go ahead
+constexpr int kShip6Stream = 2;             // per-step streams for uniform long tiles, sorted step-packed otherwise
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -515,16 +522,124 @@ __device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
     return ((uint64_t)(m.packed >> 20) << 36) | ((uint64_t)m.rel << 4);
 }
 
+
+// Sorted, step-packed row streams (echo_kernel6 with STREAM 1).  The tile's frames are ranked by their
+// row-load count (ascending, ties by index; 64 readlane compares per lane); step s streams ranked frames
+// 4s..4s+3, one per 16-lane row, so the four frames of a step need about the same number of row-loads
+// (ragged batches waste fewer lanes), and each batch of U row-loads is packed across consecutive steps
+// by a wave-uniform cursor (short frames share one round trip instead of paying one per step).  The
+// IPv4 header sum is taken in the header phase from the LDS window (header_phase5<.., IPH = true>).
+template <int U, bool FAST>
+__device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
+                                                   const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
+                                                   uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < 64u; ++j) {
+        const uint32_t nj = rdlane(nit_own, j);
+        rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
+    }
+    sort[rank] = lane;                                    // sort[0..63]: frame of rank r
+    if ((rank & 3u) == 3u) sort[64u + (rank >> 2)] = nit_own;  // sort[64 + s]: row-loads of step s
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t stepns = sort[64u + (lane & 15u)];     // lane s (< 16): row-loads of step s
+    uint32_t s = 0, j = 0;
+    while (s < 16u && rdlane(stepns, s) == 0u) ++s;
+    uint32_t cur = 16u, cur_f = 0u;
+    uint64_t ic = 0;
+    uint32_t cs = 16u, cf = 0u, crel = 0u, clim = 0u, crowhi = 0u, coff = 0u;  // metadata of step cs (per row)
+    uint64_t ca16 = 0;
+    while (s < 16u) {
+        u32x4 v[U];
+        uint32_t us[U], uj[U], uf[U], urowhi[U], ulim[U], uoff[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // wave-uniform slot assignment
+            us[u] = s;
+            uj[u] = j;
+            if (s < 16u) {
+                if (++j >= rdlane(stepns, s)) {
+                    ++s;
+                    j = 0;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (us[u] < 16u && us[u] != cs) {  // uniform: this slot starts a new step -> its rows' metadata
+                cs = us[u];
+                cf = sort[4u * cs + q];
+                const FrameMeta6 fm = meta[cf];
+                crel = fm.rel;
+                clim = fm.lim;
+                crowhi = fm.rowhi;
+                coff = fm.packed & 0xFFu;
+                if (!FAST) ca16 = meta6_a16(fm);
+            }
+            uf[u] = cf;
+            urowhi[u] = crowhi;
+            ulim[u] = clim;
+            uoff[u] = coff;
+            if (us[u] < 16u) {
+                const uint32_t ro = 256u * uj[u] + 16u * k;
+                const bool in = ro < clim;
+                if (FAST) {
+                    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(in ? crel + ro : 0x80000000u), 0, kAuxNT);
+                } else {
+                    const u32x4 y = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? ca16 + ro : 0ull)));
+                    v[u] = in ? y : u32x4{0u, 0u, 0u, 0u};
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (us[u] >= 16u) continue;  // uniform
+            if (us[u] != cur) {          // uniform: a new step begins in this slot
+                if (cur < 16u) {
+                    const uint32_t r = row_sum_dpp(fold64(ic));
+                    if (k == 15u) sums_ic[cur_f] = r;
+                }
+                cur = us[u];
+                cur_f = uf[u];
+                ic = 0;
+            }
+            const uint32_t ro = 256u * uj[u] + 16u * k;
+            const u32x4 x = v[u];
+            if (uj[u] == 0u) {
+                if (k < 4u && ulim[u]) *(u32x4*)(rows + uf[u] * kWin + ro) = x;  // the 64-B header window
+                ic += sum_range(x, (int)ro, (int)uoff[u] + 34, (int)urowhi[u]);
+            } else {
+                const int nb = (int)(urowhi[u] - min(ro, urowhi[u]));
+                u32x4 y = x;
+                y.x &= dw_mask(nb);
+                y.y &= dw_mask(nb - 4);
+                y.z &= dw_mask(nb - 8);
+                y.w &= dw_mask(nb - 12);
+                ic += sum_dw(y);
+            }
+        }
+    }
+    if (cur < 16u) {
+        const uint32_t r = row_sum_dpp(fold64(ic));
+        if (k == 15u) sums_ic[cur_f] = r;
+    }
+}
+
 // SYNC: how a wave enters its write phase.  0: at once; 1: workgroup barrier (all waves read, then
 // all write); 2: a wave whose tiles averaged >= kHeavyLen bytes per frame waits until every wave of
 // the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
 // phase separation pays where reads dominate, and costs latency hiding where frames are short.
 constexpr uint32_t kHeavyLen = 1024;
-template <int U, int TPW, int SYNC = 1>
+// STREAM: 0 = per-step row streams (stream_frame), 1 = sorted step-packed streams (stream_tile_sorted),
+// 2 = per tile: per-step streams when every parsed frame needs the same number (>= U) of row-loads
+// (uniform long frames: nothing to sort, every step fills a batch), sorted step-packed streams otherwise.
+template <int U, int TPW, int SYNC = 1, int STREAM = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kWin];  // 128 KiB at TPW 2
     __shared__ __attribute__((aligned(16))) FrameMeta6 s_meta[kWaves6][kTile];          // 16 KiB
     __shared__ uint32_t s_sum[kWaves6][2][kTile];                                        // 8 KiB
+    __shared__ uint32_t s_sort[STREAM >= 1 ? kWaves6 : 1][80];                          // 5 KiB (STREAM 1, 2)
     __shared__ unsigned long long s_cnt[kWaves6][4];
     __shared__ uint32_t s_arrive;
     if (SYNC == 2) {
@@ -632,6 +747,11 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                             sums_ip[f] = rip;
                         }
                     }
+                } else if (STREAM == 1 ||
+                           (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
+                                            uniform(max_nit_lane(nit)) < (uint32_t)U))) {
+                    if (fast) stream_tile_sorted<U, true>(a, ld.r, meta, s_sort[STREAM >= 1 ? wave : 0], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted<U, false>(a, ld.r, meta, s_sort[STREAM >= 1 ? wave : 0], rows, sums_ic, nit, lane);
                 } else {
                     for (uint32_t s = 0; s < 16; ++s) {
                         const uint32_t f = 4u * s + q;
@@ -667,8 +787,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             __builtin_amdgcn_wave_barrier();
             const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
             const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
-            const bool wb = header_phase5<true>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, fi < a.n, ok,
-                                                parse, fi, cnt, &rec[i], &verd[i]);
+            const bool wb = header_phase5<true, STREAM >= 1>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len,
+                                                             fi < a.n, ok, parse, fi, cnt, &rec[i], &verd[i]);
             wbm[i] = __ballot(wb);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();  // meta/sums are rewritten by the next tile

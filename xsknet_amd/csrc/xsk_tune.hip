@@ -364,6 +364,11 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 70: echo_kernel6<4, 2, 0><<<gg, bb, 0, s>>>(args, per); break;
             case 71: echo_kernel6<4, 1, 0><<<gg, bb, 0, s>>>(args, per); break;
             case 72: echo_kernel6<4, 2, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 73: echo_kernel6<4, 2, 2, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 74: echo_kernel6<6, 2, 2, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 75: echo_kernel6<8, 2, 2, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 76: echo_kernel6<4, 2, 2, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 77: echo_kernel6<6, 2, 2, 2><<<gg, bb, 0, s>>>(args, per); break;
             default: return -EINVAL;
         }
         HIP_TRY(hipGetLastError());
