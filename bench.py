@@ -33,7 +33,11 @@ CONFIGS = {
     "c3": (1 << 20, 1500, 1500, 4096, 0x5EED0003,
            "c3: 1M x 1500B ICMP echo frames, 4 KiB UMEM-chunk stride, full-payload checksum"),
     "c4": (1 << 20, 64, 1500, 2048, 0x5EED0004, "c4: 1M x U{64..1500}B ICMP echo frames, 2 KiB stride"),
+    # C5 is a STRONG-scaling config: 64 M frames in total per step, frame i on GPU i mod N
+    "c5": (1 << 26, 1500, 1500, 2048, 0x5EED0005,
+           "c5: 64M x 1500B ICMP echo frames per step in total, round-robin over the GPUs, 2 KiB stride"),
 }
+STRONG = {"c5"}
 
 
 def log(*a):
@@ -188,6 +192,10 @@ def main():
     rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", local)
     n, lo, hi, stride, seed, desc = CONFIGS[args.config]
+    if args.config in STRONG:  # fixed total work split over the ranks
+        if n % world:
+            raise SystemExit(f"{args.config}: {n} frames do not split over {world} ranks")
+        n //= world
     kernel = KERNEL if args.opts == 0 else WIRE_KERNEL
     if args.opts:
         desc += f"; wire-format options {args.opts:#x} (xsk_gpu_echo_dev_opts)"
@@ -292,7 +300,7 @@ def main():
             "warmup": W,
             "ms_per_step": round(wall_max / K * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config in STRONG else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded counter-based ICMP echo requests generated on-GPU, bit-identical "

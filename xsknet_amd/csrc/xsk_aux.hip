@@ -208,8 +208,17 @@ int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_d
     a.mode = mode;
     a.len_lo = len_lo;
     a.len_hi = len_hi;
-    hipLaunchKernelGGL(synth_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, a);
-    HIP_TRY(hipGetLastError());
+    // at most 4 M frames (1 M workgroups) per launch: a grid's thread count must stay below 2^32
+    constexpr uint32_t kChunk = 1u << 22;
+    for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+        SynthArgs b = a;
+        b.n = n - c0 < kChunk ? n - c0 : kChunk;
+        b.descs = d_descs + c0;
+        b.base_off = base_off + (uint64_t)c0 * stride;
+        b.first = first + (uint64_t)c0 * step;
+        hipLaunchKernelGGL(synth_kernel, dim3((b.n + 3) / 4), dim3(256), 0, (hipStream_t)stream, b);
+        HIP_TRY(hipGetLastError());
+    }
     return 0;
 }
 

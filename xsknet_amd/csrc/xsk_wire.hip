@@ -7,7 +7,9 @@
 // comment block above XSK_GPU_OPT_STRICT_IPV4 in include/xsk_gpu.h; oracle_echo_batch_opts() restates it
 // on the CPU.
 //
-// Layout: one wave per 64-frame tile, lane = frame.  Each lane loads its frame's 128-B header window
+// Layout: the round structure of echo_kernel6 (one 16-wave workgroup per CU, one tile per wave per
+// round, heavy waves write after the round; see the template comment).  One wave per 64-frame tile,
+// lane = frame.  Each lane loads its frame's 128-B header window
 // (16-B aligned, 8 x 16 B) into an LDS row, parses it with byte reads, and sums the IPv4 header and the
 // part of the ICMP message inside the window from LDS (absolute-alignment domain, like the round
 // kernel).  The rest of the message, row bytes [128, off + end), is streamed by 16-lane rows (one frame
@@ -29,32 +31,52 @@ __device__ __forceinline__ uint32_t be16_at(const uint8_t* row, uint32_t i) {
     return ((uint32_t)row[i] << 8) | (uint32_t)row[i + 1];
 }
 
-template <int U>
-__global__ __launch_bounds__(kThreads) void echo_wire_kernel(EchoArgs a, uint32_t opts) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_row[kWaves][kTile * kWinW];  // 32 KiB
-    __shared__ uint64_t s_a16[kWaves][kTile];
-    __shared__ uint32_t s_hi[kWaves][kTile];   // row coordinate of the message end when it passes the window
-    __shared__ uint32_t s_sum[kWaves][kTile];  // streamed part of the ICMP sum (row-reduced)
-    __shared__ unsigned long long s_cnt[kWaves][4];
+// NW waves per workgroup.  ROUND = false: a grid of small workgroups, each wave a tile at a time,
+// writes at the tile's end.  ROUND = true: the round structure of echo_kernel6 (one 16-wave workgroup
+// per CU, equal contiguous tile shares, one tile per wave per round); a wave whose tile averaged
+// >= kHeavyLen bytes per frame holds its header sectors, records and verdicts until every wave of the
+// workgroup has finished reading the round, so HBM sees read phases and write bursts, not a mix.
+template <int U, int NW, bool ROUND>
+__global__ __launch_bounds__(NW * 64) void echo_wire_kernel(EchoArgs a, uint32_t opts, uint32_t tiles_per_wg) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_row[NW][kTile * kWinW];  // 8 KiB per wave
+    __shared__ uint64_t s_a16[NW][kTile];
+    __shared__ uint32_t s_hi[NW][kTile];   // row coordinate of the message end when it passes the window
+    __shared__ uint32_t s_sum[NW][kTile];  // streamed part of the ICMP sum (row-reduced)
+    __shared__ unsigned long long s_cnt[NW][4];
+    __shared__ uint32_t s_arrive;
+    if (ROUND) {
+        if (threadIdx.x == 0) s_arrive = 0u;
+        __syncthreads();
+    }
 
     const uint32_t wave = uniform(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t q = lane >> 4, k = lane & 15u;
     uint8_t* rows = s_row[wave];
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
-    const uint32_t nwaves = gridDim.x * kWaves;
     const bool strict = (opts & XSK_GPU_OPT_STRICT_IPV4) != 0u;
     const bool vlan = (opts & XSK_GPU_OPT_VLAN) != 0u;
     const bool verify = (opts & XSK_GPU_OPT_VERIFY_CSUM) != 0u;
     Counters cnt;
+    // tile loop: ROUND -> workgroup-uniform rounds over the share [t_begin, t_end); else grid-stride
+    const uint32_t t_begin = ROUND ? blockIdx.x * tiles_per_wg : blockIdx.x * NW + wave;
+    const uint32_t t_end = ROUND ? min(ntiles, t_begin + tiles_per_wg) : ntiles;
+    const uint32_t t_step = ROUND ? (uint32_t)NW : gridDim.x * NW;
+    uint32_t rounds_done = 0;
 
-    for (uint32_t t = blockIdx.x * kWaves + wave; t < ntiles; t += nwaves) {
-        // ---- descriptor (xsk_receive.c:222-223) and the 128-B window -> LDS row ------------------
+    for (uint32_t it = t_begin; it < t_end; it += t_step) {
+        const uint32_t t = ROUND ? it + wave : it;
+        const bool have = t < t_end;  // wave-uniform (always true without ROUND)
+        uint64_t wbm = 0;
+        uint32_t verdict = XSK_GPU_TX_REPLY, len = 0;
+        u32x4 recv = u32x4{0u, 0u, 0u, 0u};
         const uint32_t fi = t * kTile + lane;
+        if (have) {
+        // ---- descriptor (xsk_receive.c:222-223) and the 128-B window -> LDS row ------------------
         u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
         if (fi < a.n) dsc = *(const u32x4*)(a.descs + fi);
         const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
-        const uint32_t len = dsc.z;
+        len = dsc.z;
         const bool ok = fi < a.n && len <= kMaxLen && addr <= a.umem_size && len <= a.umem_size - addr;
         const uint64_t a16 = addr & ~15ull;
         const uint32_t off = (uint32_t)addr & 15u;
@@ -73,7 +95,6 @@ __global__ __launch_bounds__(kThreads) void echo_wire_kernel(EchoArgs a, uint32_
 
         // ---- parse (spec: include/xsk_gpu.h, XSK_GPU_OPT_*) ----------------------------------------
         const uint8_t* p = row + off;  // frame byte i = p[i] for i < wend - off
-        uint32_t verdict = XSK_GPU_TX_REPLY;
         uint32_t l3 = 14, hl = 20, end = len, et = 0, tags = 0;
         bool hdrs = false;  // all three headers inside the frame: the record is filled
         if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
@@ -230,29 +251,15 @@ __global__ __launch_bounds__(kThreads) void echo_wire_kernel(EchoArgs a, uint32_
                 pkt[l4 + 3] = w[l4 + 3];
             }
         }
-        const uint64_t wbm = __ballot(wb);
-        if (wbm) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
-                const uint32_t kk = lane & 3u;
-                if ((wbm >> f) & 1ull)
-                    *(u32x4*)(a.umem + s_a16[wave][f] + 16u * kk) = *(const u32x4*)(rows + f * kWinW + 16u * kk);
-            }
+        wbm = __ballot(wb);
+        {
+            const uint32_t vihl = hdrs ? p[l3] : 0u, proto = hdrs ? 1u : 0u;
+            recv.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+            recv.y = icode | (vihl << 8) | ((hdrs ? et : 0u) << 16);
+            recv.z = csum_in | (csum_out << 16);
+            recv.w = (hdrs ? ip_sum : 0u) | ((hdrs ? ic_sum : 0u) << 16);
         }
         if (fi < a.n) {
-            if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
-            if (a.recs) {
-                u32x4 r;
-                const uint32_t vihl = hdrs ? p[l3] : 0u, proto = hdrs ? 1u : 0u;
-                r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
-                r.y = icode | (vihl << 8) | ((hdrs ? et : 0u) << 16);
-                r.z = csum_in | (csum_out << 16);
-                r.w = (hdrs ? ip_sum : 0u) | ((hdrs ? ic_sum : 0u) << 16);
-                ((u32x4*)a.recs)[fi] = r;
-            }
             cnt.rxp += 1;
             cnt.rxb += len;
             if (tx) {
@@ -260,21 +267,56 @@ __global__ __launch_bounds__(kThreads) void echo_wire_kernel(EchoArgs a, uint32_
                 cnt.txb += len;
             }
         }
+        }  // have
+        if (ROUND) {  // heavy waves wait until the whole workgroup has read this round
+            ++rounds_done;
+            const uint32_t bytes = uniform(wave_sum_u32(have && fi < a.n ? min(len, 65536u) : 0u));
+            if (lane == 0) atomicAdd(&s_arrive, 1u);
+            if (bytes >= kHeavyLen * kTile) {
+                while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                       rounds_done * (uint32_t)NW)
+                    __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (have) {
+            if (wbm) {  // patched 64-B sectors, 16 frames per wave-store
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                    const uint32_t kk = lane & 3u;
+                    if ((wbm >> f) & 1ull)
+                        *(u32x4*)(a.umem + s_a16[wave][f] + 16u * kk) = *(const u32x4*)(rows + f * kWinW + 16u * kk);
+                }
+            }
+            if (fi < a.n) {
+                if (a.verdicts) a.verdicts[fi] = (uint8_t)verdict;
+                if (a.recs) ((u32x4*)a.recs)[fi] = recv;
+            }
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next tile
     }
-    store_partials(a, cnt, s_cnt, wave, lane);
+    store_partials<NW>(a, cnt, s_cnt, wave, lane);
 }
 
 }  // namespace
 
 extern "C" {
 
+uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip
+
 // Internal: wire-mode launch (xsk_gpu_echo_dev_opts in xsk_echo.hip validates the arguments).
 int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                            uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, void* d_partials,
                            uint32_t* grid_out, void* stream) {
-    const uint32_t grid = echo_grid(n);
+    int device = 0;
+    HIP_TRY(hipGetDevice(&device));
+    const uint32_t ncu = xsk_gpu__num_cu(device);
+    if (!ncu) return xsk_gpu__hip_fail(hipErrorInvalidDevice);
+    uint32_t grid = 0, tiles_per_wg = 0;
+    echo6_geometry(n, ncu, &grid, &tiles_per_wg);
     EchoArgs args;
     args.umem = (uint8_t*)d_umem;
     args.umem_size = umem_size;
@@ -283,7 +325,8 @@ int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gp
     args.verdicts = d_verdicts;
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_partials;
-    echo_wire_kernel<kWireU><<<dim3(grid), dim3(kThreads), 0, (hipStream_t)stream>>>(args, opts);
+    echo_wire_kernel<kWireU, kWaves6, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, opts,
+                                                                                                   tiles_per_wg);
     HIP_TRY(hipGetLastError());
     *grid_out = grid;
     return 0;
