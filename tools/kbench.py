@@ -92,6 +92,17 @@ def main():
                     if rep > 0:
                         times[(v, g)].extend(evs)
             torch.cuda.synchronize()
+        if 79 in variants:  # per-workgroup start/end wall clock of the last launch (workspace tail)
+            torch.cuda.synchronize()
+            t = ws.view(torch.int64)[8192:8192 + 2 * 256].cpu().view(256, 2).double() / 100.0  # us
+            t0 = t[:, 0].min()
+            st, en = t[:, 0] - t0, t[:, 1] - t0
+            print(json.dumps({"layout": lname, "wg_timing": True, "start_max": round(float(st.max()), 1),
+                              "end_min": round(float(en.min()), 1), "end_med": round(float(en.median()), 1),
+                              "end_max": round(float(en.max()), 1),
+                              "end_mean_per_xcd": [round(float(en[x::8].mean()), 1) for x in range(8)],
+                              "end_sorted_deciles": [round(float(en.sort().values[min(255, int(i * 25.6))]), 1)
+                                                     for i in range(11)]}), flush=True)
         for (v, g), evs in times.items():
             ms = sorted(a.elapsed_time(b) for a, b in evs)
             med = ms[len(ms) // 2]

@@ -626,6 +626,128 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
     }
 }
 
+
+// stream_tile_sorted with the batches software-pipelined: batch b+1's U row-loads are issued before
+// batch b is consumed, so 1-2 batches stay in flight per lane instead of draining to zero at every
+// batch end.  The consume side re-reads each slot's frame metadata from LDS (issued under the loads).
+template <int U>
+struct SortedBatch {
+    u32x4 v[U];
+    uint32_t s[U], j[U], f[U];  // s, j wave-uniform; f per 16-lane row
+};
+
+template <int U, bool FAST>
+__device__ __forceinline__ void sp_issue(SortedBatch<U>& B, uint32_t& s, uint32_t& j, uint32_t stepns,
+                                         uint32_t& cs, uint32_t& cf, uint32_t& crel, uint32_t& clim, uint64_t& ca16,
+                                         const uint32_t* sort, const FrameMeta6* meta, __amdgpu_buffer_rsrc_t rsrc,
+                                         const EchoArgs& a, uint32_t q, uint32_t k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // wave-uniform slot assignment
+        B.s[u] = s;
+        B.j[u] = j;
+        if (s < 16u) {
+            if (++j >= rdlane(stepns, s)) {
+                ++s;
+                j = 0;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        B.v[u] = u32x4{0u, 0u, 0u, 0u};
+        if (B.s[u] < 16u) {
+            if (B.s[u] != cs) {  // uniform: the slot starts a new step
+                cs = B.s[u];
+                cf = sort[4u * cs + q];
+                const FrameMeta6 fm = meta[cf];
+                crel = fm.rel;
+                clim = fm.lim;
+                if (!FAST) ca16 = meta6_a16(fm);
+            }
+            const uint32_t ro = 256u * B.j[u] + 16u * k;
+            const bool in = ro < clim;
+            if (FAST) {
+                B.v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(in ? crel + ro : 0x80000000u), 0, kAuxNT);
+            } else {
+                const u32x4 y = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? ca16 + ro : 0ull)));
+                B.v[u] = in ? y : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+        B.f[u] = cf;
+    }
+}
+
+template <int U>
+__device__ __forceinline__ void sp_consume(const SortedBatch<U>& B, uint32_t& cur, uint32_t& cur_f, uint64_t& ic,
+                                           const FrameMeta6* meta, uint8_t* rows, uint32_t* sums_ic, uint32_t k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (B.s[u] >= 16u) continue;  // uniform
+        if (B.s[u] != cur) {          // uniform: a new step begins in this slot
+            if (cur < 16u) {
+                const uint32_t r = row_sum_dpp(fold64(ic));
+                if (k == 15u) sums_ic[cur_f] = r;
+            }
+            cur = B.s[u];
+            cur_f = B.f[u];
+            ic = 0;
+        }
+        const FrameMeta6 fm = meta[B.f[u]];
+        const uint32_t rowhi = fm.rowhi, off = fm.packed & 0xFFu;
+        const uint32_t ro = 256u * B.j[u] + 16u * k;
+        const u32x4 x = B.v[u];
+        if (B.j[u] == 0u) {
+            if (k < 4u) *(u32x4*)(rows + B.f[u] * kWin + ro) = x;  // the 64-B header window
+            ic += sum_range(x, (int)ro, (int)off + 34, (int)rowhi);
+        } else {
+            const int nb = (int)(rowhi - min(ro, rowhi));
+            u32x4 y = x;
+            y.x &= dw_mask(nb);
+            y.y &= dw_mask(nb - 4);
+            y.z &= dw_mask(nb - 8);
+            y.w &= dw_mask(nb - 12);
+            ic += sum_dw(y);
+        }
+    }
+}
+
+template <int U, bool FAST>
+__device__ __forceinline__ void stream_tile_sorted_pl(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
+                                                      const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
+                                                      uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < 64u; ++j) {
+        const uint32_t nj = rdlane(nit_own, j);
+        rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
+    }
+    sort[rank] = lane;
+    if ((rank & 3u) == 3u) sort[64u + (rank >> 2)] = nit_own;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t stepns = sort[64u + (lane & 15u)];
+    uint32_t s = 0, j = 0;
+    while (s < 16u && rdlane(stepns, s) == 0u) ++s;
+    uint32_t cs = 16u, cf = 0u, crel = 0u, clim = 0u;
+    uint64_t ca16 = 0;
+    uint32_t cur = 16u, cur_f = 0u;
+    uint64_t ic = 0;
+    SortedBatch<U> A, B;
+    sp_issue<U, FAST>(A, s, j, stepns, cs, cf, crel, clim, ca16, sort, meta, rsrc, a, q, k);
+    while (true) {  // ping-pong: issue the next batch, then consume the older one
+        if (A.s[0] >= 16u) break;
+        sp_issue<U, FAST>(B, s, j, stepns, cs, cf, crel, clim, ca16, sort, meta, rsrc, a, q, k);
+        sp_consume<U>(A, cur, cur_f, ic, meta, rows, sums_ic, k);
+        if (B.s[0] >= 16u) break;
+        sp_issue<U, FAST>(A, s, j, stepns, cs, cf, crel, clim, ca16, sort, meta, rsrc, a, q, k);
+        sp_consume<U>(B, cur, cur_f, ic, meta, rows, sums_ic, k);
+    }
+    if (cur < 16u) {
+        const uint32_t r = row_sum_dpp(fold64(ic));
+        if (k == 15u) sums_ic[cur_f] = r;
+    }
+}
+
 // SYNC: how a wave enters its write phase.  0: at once; 1: workgroup barrier (all waves read, then
 // all write); 2: a wave whose tiles averaged >= kHeavyLen bytes per frame waits until every wave of
 // the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
@@ -633,9 +755,15 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
 constexpr uint32_t kHeavyLen = 1024;
 // STREAM: 0 = per-step row streams (stream_frame), 1 = sorted step-packed streams (stream_tile_sorted),
 // 2 = per tile: per-step streams when every parsed frame needs the same number (>= U) of row-loads
-// (uniform long frames: nothing to sort, every step fills a batch), sorted step-packed streams otherwise.
-template <int U, int TPW, int SYNC = 1, int STREAM = 0>
+// (uniform long frames: nothing to sort, every step fills a batch), sorted step-packed streams otherwise;
+// 3 = sorted step-packed streams with software-pipelined batches (stream_tile_sorted_pl) for every
+// tile; 4 = as 2 with the pipelined version.
+// PF: load the descriptors of the wave's next tile while the current one streams.
+// WGT (tuning only): record each workgroup's start / end wall clock (100 MHz) after the counter
+// partials in the workspace (u64 [8192 + 2 g], [8192 + 2 g + 1]).
+template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
+    const uint64_t wgt_start = WGT ? wall_clock64() : 0ull;
     __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kWin];  // 128 KiB at TPW 2
     __shared__ __attribute__((aligned(16))) FrameMeta6 s_meta[kWaves6][kTile];          // 16 KiB
     __shared__ uint32_t s_sum[kWaves6][2][kTile];                                        // 8 KiB
@@ -658,6 +786,11 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
     constexpr uint32_t kRound = (uint32_t)kWaves6 * TPW;
     Counters cnt;
     uint32_t lane = threadIdx.x & 63u;
+    u32x4 dnext = u32x4{0u, 0u, 0u, 0u};  // PF: descriptor of this lane's frame in the wave's next tile
+    if (PF) {
+        const uint32_t f0 = (t_begin + wave) * kTile + lane;
+        if (t_begin + wave < t_end && f0 < a.n) dnext = *(const u32x4*)(a.descs + f0);
+    }
 
     for (uint32_t r0 = t_begin; r0 < t_end; r0 += kRound) {  // workgroup-uniform
         u32x4 rec[TPW];
@@ -680,7 +813,15 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             const uint32_t fi = t * kTile + lane;
             // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
             u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
-            if (fi < a.n) dsc = *(const u32x4*)(a.descs + fi);
+            if (PF) {
+                dsc = dnext;
+                const uint32_t tn = i + 1 < TPW ? t + (uint32_t)kWaves6 : r0 + kRound + wave;  // next tile
+                const uint32_t fn = tn * kTile + lane;
+                dnext = u32x4{0u, 0u, 0u, 0u};
+                if (tn < t_end && fn < a.n) dnext = *(const u32x4*)(a.descs + fn);
+            } else if (fi < a.n) {
+                dsc = *(const u32x4*)(a.descs + fi);
+            }
             const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
             const uint32_t len = dsc.z;
             const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
@@ -747,11 +888,16 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                             sums_ip[f] = rip;
                         }
                     }
+                } else if (STREAM == 3 ||
+                           (STREAM == 4 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
+                                            uniform(max_nit_lane(nit)) < (uint32_t)U))) {
+                    if (fast) stream_tile_sorted_pl<U, true>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted_pl<U, false>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else if (STREAM == 1 ||
                            (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                             uniform(max_nit_lane(nit)) < (uint32_t)U))) {
-                    if (fast) stream_tile_sorted<U, true>(a, ld.r, meta, s_sort[STREAM >= 1 ? wave : 0], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted<U, false>(a, ld.r, meta, s_sort[STREAM >= 1 ? wave : 0], rows, sums_ic, nit, lane);
+                    if (fast) stream_tile_sorted<U, true>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted<U, false>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else {
                     for (uint32_t s = 0; s < 16; ++s) {
                         const uint32_t f = 4u * s + q;
@@ -833,6 +979,10 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next round
     }
     store_partials<kWaves6>(a, cnt, s_cnt, wave, lane);
+    if (WGT && threadIdx.x == 0 && a.partials) {
+        a.partials[8192 + 2 * blockIdx.x] = wgt_start;
+        a.partials[8192 + 2 * blockIdx.x + 1] = wall_clock64();
+    }
 }
 
 

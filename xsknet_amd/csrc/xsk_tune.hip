@@ -344,7 +344,7 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_workspace;
     hipStream_t s = (hipStream_t)stream;
-    if (variant >= 60 && variant < 80) {  // round kernel: max_grid = workgroups (0: one per CU)
+    if (variant >= 60 && variant < 90) {  // round kernel: max_grid = workgroups (0: one per CU)
         int device = 0;
         HIP_TRY(hipGetDevice(&device));
         uint32_t g6 = 0, per = 0;
@@ -369,6 +369,12 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 75: echo_kernel6<8, 2, 2, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 76: echo_kernel6<4, 2, 2, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 77: echo_kernel6<6, 2, 2, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 78: echo_kernel6<4, 2, 2, 2, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 79: echo_kernel6<4, 2, 2, 2, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 80: echo_kernel6<4, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
+            case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
+            case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
+            case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             default: return -EINVAL;
         }
         HIP_TRY(hipGetLastError());
