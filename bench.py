@@ -26,7 +26,7 @@ import torch  # noqa: E402
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 KERNEL = "echo_kernel6<4, 2, 2, 2, false, false>"  # the transform kernel xsk_gpu_echo_dev launches
-WIRE_KERNEL = "echo_wire_kernel<4, 16, true>"  # xsk_gpu_echo_dev_opts with nonzero options (--opts)
+WIRE_KERNEL = "echo_kernel6<4, 1, 2, 2, false, false, true>"  # xsk_gpu_echo_dev_opts, nonzero --opts
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
@@ -188,6 +188,10 @@ def main():
     import xsknet_amd as X
     from xsknet_amd import shard
     X.lib()  # fail loudly if the HIP library is missing
+    if os.environ.get("XSK_WIRE_IMPL"):  # tuning only: 1 = the window-first wire kernel, for comparison
+        import ctypes
+        X.lib().xsk_gpu__set_wire_impl.argtypes = [ctypes.c_int]
+        assert X.lib().xsk_gpu__set_wire_impl(int(os.environ["XSK_WIRE_IMPL"])) == 0
 
     rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", local)

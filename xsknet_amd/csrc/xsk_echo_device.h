@@ -30,6 +30,7 @@ struct EchoArgs {
     uint8_t* verdicts;
     xsk_gpu_rec* recs;
     unsigned long long* partials;  // [gridDim.x][4]: rx_packets, rx_bytes, tx_packets, tx_bytes
+    uint32_t opts = 0;             // XSK_GPU_OPT_* (wire-mode kernels only)
 };
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -160,16 +161,20 @@ struct FrameMeta {
 // first row-load carries the 64-B window: lanes 0-3 drop it into the frame's LDS row and every lane
 // sums its bytes by exact range (ICMP [off+34, rowhi), IPv4 header [off+14, iphi)); later blocks only
 // need the frame-end mask.
-template <int U, class L>
+// WIRE (wire-format mode): the window is 128 B (lanes 0-7) and the stream sums only row bytes
+// [128, rowhi) -- the parse, and so the ICMP start and end, are known only in the header phase, which
+// sums the in-window part from LDS (wire_header_phase).
+template <int U, class L, bool WIRE = false>
 __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t f_rowhi, uint32_t f_lim,
                                              uint32_t f_off, uint32_t f_iphi, uint32_t k, uint8_t* hdr_row,
                                              RowSums& rs) {
+    const int ic_lo = WIRE ? 128 : (int)f_off + 34;
     if (ns == 1u) {
         const uint32_t ro = 16u * k;
         const u32x4 x = ld.load(ro, ro < f_lim);
-        if (k < 4u) *(u32x4*)(hdr_row + ro) = x;
-        rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
-        rs.ic += sum_range(x, (int)ro, (int)f_off + 34, (int)f_rowhi);
+        if (k < (WIRE ? 8u : 4u)) *(u32x4*)(hdr_row + ro) = x;
+        if (!WIRE) rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
+        rs.ic += sum_range(x, (int)ro, ic_lo, (int)f_rowhi);
         return;
     }
     for (uint32_t j0 = 0; j0 < ns; j0 += U) {
@@ -184,9 +189,9 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
             const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
             const u32x4 x = v[u];
             if (u == 0 && j0 == 0u) {
-                if (k < 4u) *(u32x4*)(hdr_row + ro) = x;
-                rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
-                rs.ic += sum_range(x, (int)ro, (int)f_off + 34, (int)f_rowhi);
+                if (k < (WIRE ? 8u : 4u)) *(u32x4*)(hdr_row + ro) = x;
+                if (!WIRE) rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
+                rs.ic += sum_range(x, (int)ro, ic_lo, (int)f_rowhi);
             } else {
                 const int nb = (int)(f_rowhi - min(ro, f_rowhi));      // frame bytes in this block
                 if (__ballot(nb > 0 && nb < 16) != 0ull) {             // a block that ends a frame
@@ -529,10 +534,11 @@ __device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
 // (ragged batches waste fewer lanes), and each batch of U row-loads is packed across consecutive steps
 // by a wave-uniform cursor (short frames share one round trip instead of paying one per step).  The
 // IPv4 header sum is taken in the header phase from the LDS window (header_phase5<.., IPH = true>).
-template <int U, bool FAST>
+template <int U, bool FAST, bool WIRE = false>
 __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
                                                    const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
                                                    uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
+    constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (window) bytes
     const uint32_t q = lane >> 4, k = lane & 15u;
     uint32_t rank = 0;
     for (uint32_t j = 0; j < 64u; ++j) {
@@ -607,8 +613,8 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
             const uint32_t ro = 256u * uj[u] + 16u * k;
             const u32x4 x = v[u];
             if (uj[u] == 0u) {
-                if (k < 4u && ulim[u]) *(u32x4*)(rows + uf[u] * kWin + ro) = x;  // the 64-B header window
-                ic += sum_range(x, (int)ro, (int)uoff[u] + 34, (int)urowhi[u]);
+                if (k < kRowW / 16u && ulim[u]) *(u32x4*)(rows + uf[u] * kRowW + ro) = x;  // the header window
+                ic += sum_range(x, (int)ro, WIRE ? 128 : (int)uoff[u] + 34, (int)urowhi[u]);
             } else {
                 const int nb = (int)(urowhi[u] - min(ro, urowhi[u]));
                 u32x4 y = x;
@@ -748,6 +754,168 @@ __device__ __forceinline__ void stream_tile_sorted_pl(const EchoArgs& a, __amdgp
     }
 }
 
+
+// ================================================================================================
+// Wire-format header phase (xsk_gpu_echo_dev_opts; spec: include/xsk_gpu.h).
+// Lane = frame.  `row` is the frame's 16-B aligned 128-B window in LDS (frame byte i at row[off + i]),
+// `far_raw` the stream's folded sum of row bytes [128, off + len) (absolute-alignment domain).  Parses
+// VLAN tags / IHL / tot_len / fragments, sums the IPv4 header and the in-window part of the ICMP message
+// from LDS, completes the message sum (re-reading [128, off + end) from memory in the rare case that
+// STRICT cuts a message short of the frame beyond the window), decides, patches the reply in LDS.
+// Returns true when the patched 64-B window should leave as a whole sector (aligned, rewrite < 64 B).
+// ================================================================================================
+__device__ __forceinline__ uint32_t wbe16(const uint8_t* p, uint32_t i) {
+    return ((uint32_t)p[i] << 8) | (uint32_t)p[i + 1];
+}
+
+__device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* row, uint32_t far_raw, uint64_t addr,
+                                                  uint32_t len, bool ok, bool live, uint32_t wend, Counters& cnt,
+                                                  u32x4* rec_out, uint32_t* verd_out) {
+    const bool strict = (a.opts & XSK_GPU_OPT_STRICT_IPV4) != 0u;
+    const bool vlan = (a.opts & XSK_GPU_OPT_VLAN) != 0u;
+    const bool verify = (a.opts & XSK_GPU_OPT_VERIFY_CSUM) != 0u;
+    const uint32_t off = (uint32_t)addr & 15u;
+    uint8_t* p = row + off;  // frame byte i = p[i] for off + i < wend
+    uint32_t verdict = XSK_GPU_TX_REPLY;
+    uint32_t l3 = 14, hl = 20, end = len, et = 0, tags = 0;
+    bool hdrs = false;  // all three headers inside the frame: the record is filled
+    if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+    else if (len < 14) verdict = XSK_GPU_DROP_SHORT;
+    else {
+        et = wbe16(p, 12);
+        bool cut = false;
+        if (vlan) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                if (!cut && (et == 0x8100u || et == 0x88A8u) && tags == (uint32_t)g) {
+                    if (len < l3 + 4) cut = true;
+                    else {
+                        et = wbe16(p, l3 + 2);
+                        l3 += 4;
+                        tags++;
+                    }
+                }
+            }
+        }
+        if (cut) verdict = XSK_GPU_DROP_SHORT;
+        else if (et != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;
+        else if (len < l3 + 20) verdict = XSK_GPU_DROP_SHORT;
+        else {
+            bool bad = false;
+            if (strict) {
+                const uint32_t vihl = p[l3];
+                if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
+                else {
+                    hl = 4u * (vihl & 15u);
+                    const uint32_t tot = wbe16(p, l3 + 2);
+                    if (tot < hl + 8 || l3 + tot > len) bad = true;
+                    else if (wbe16(p, l3 + 6) & 0x3FFFu) bad = true;
+                    else end = l3 + tot;
+                }
+            }
+            if (bad) verdict = XSK_GPU_DROP_BAD_IP;
+            else if (p[l3 + 9] != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
+            else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
+            else hdrs = true;
+        }
+    }
+    const uint32_t l4 = l3 + hl;
+    uint32_t ip_sum = 0, ic_sum = 0, itype = 0, icode = 0, csum_in = 0, flags = 0;
+    if (hdrs) {
+        // in-window sums (absolute-alignment domain: LE dwords of the 16-B aligned row)
+        const uint32_t ic_end = off + end, ic_hi_w = min(ic_end, 128u);
+        uint64_t ip_acc = 0, ic_acc = 0;
+        const uint32_t* r32 = (const uint32_t*)row;
+#pragma unroll 8
+        for (int d = 0; d < 32; ++d) {
+            const uint32_t x = r32[d];
+            ip_acc += keep_bytes(x, 4 * d, (int)(off + l3), (int)(off + l4));
+            ic_acc += keep_bytes(x, 4 * d, (int)(off + l4), (int)ic_hi_w);
+        }
+        uint64_t far = 0;
+        if (ic_end > 128u) {
+            if (end == len) {
+                far = far_raw;  // the stream summed exactly [128, off + len)
+            } else {            // STRICT message ending before the frame does, beyond the window: re-read
+                const uint8_t* fb = a.umem + (addr & ~15ull);
+                for (uint32_t o = 128u; o < ic_end; o += 4u)
+                    far += keep_bytes(*(const uint32_t*)(fb + o), (int)o, 128, (int)ic_end);
+            }
+        }
+        ip_sum = fold64(ip_acc);
+        ic_sum = fold64(ic_acc + far);
+        if (!((uint32_t)addr & 1u)) {
+            ip_sum = bswap16(ip_sum);
+            ic_sum = bswap16(ic_sum);
+        }
+        itype = p[l4];
+        icode = p[l4 + 1];
+        csum_in = wbe16(p, l4 + 2);
+        if (ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
+        if (ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
+        if (tags) flags |= XSK_GPU_F_VLAN;
+        if (hl > 20u) flags |= XSK_GPU_F_IP_OPTIONS;
+        if (itype != 8u || (strict && icode != 0u)) verdict = XSK_GPU_DROP_NOT_ECHO;
+        else if (verify && (ip_sum != 0xFFFFu || ic_sum != 0xFFFFu)) verdict = XSK_GPU_DROP_BAD_CSUM;
+    }
+    const bool tx = hdrs && verdict == XSK_GPU_TX_REPLY;
+    uint32_t csum_out = csum_in;
+    bool wb = false;
+    if (tx) {
+        // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY) on the LE-loaded field (xsk_receive.c:101-111)
+        const uint32_t csum_le = ((csum_in & 0xFFu) << 8) | (csum_in >> 8);
+        uint32_t c16 = (~csum_le) & 0xFFFFu;
+        c16 = (c16 + 0xFFF7u) & 0xFFFFu;
+        c16 += c16 < 0xFFF7u ? 1u : 0u;
+        const uint32_t csum_new_le = (~c16) & 0xFFFFu;
+        csum_out = bswap16(csum_new_le);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {  // xsk_receive.c:148-157 at the parsed offsets, in LDS
+            const uint8_t x = p[i];
+            p[i] = p[6 + i];
+            p[6 + i] = x;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint8_t x = p[l3 + 12 + i];
+            p[l3 + 12 + i] = p[l3 + 16 + i];
+            p[l3 + 16 + i] = x;
+        }
+        p[l4] = 0;
+        p[l4 + 2] = (uint8_t)csum_new_le;
+        p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+        if (off == 0u && l4 + 4u <= 64u && wend >= 64u) {
+            wb = true;  // whole 64-B sector, stored in the write phase
+        } else {        // byte-exact: only the rewritten bytes
+            uint8_t* pkt = a.umem + addr;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pkt[i] = p[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
+            pkt[l4] = 0;
+            pkt[l4 + 2] = p[l4 + 2];
+            pkt[l4 + 3] = p[l4 + 3];
+        }
+    }
+    const uint32_t vihl = hdrs ? p[l3] : 0u, proto = hdrs ? 1u : 0u;
+    u32x4 r;
+    r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+    r.y = icode | (vihl << 8) | ((hdrs ? et : 0u) << 16);
+    r.z = csum_in | (csum_out << 16);
+    r.w = ip_sum | (ic_sum << 16);
+    *rec_out = r;
+    *verd_out = verdict;
+    if (live) {
+        cnt.rxp += 1;
+        cnt.rxb += len;
+        if (tx) {
+            cnt.txp += 1;
+            cnt.txb += len;
+        }
+    }
+    return wb;
+}
+
 // SYNC: how a wave enters its write phase.  0: at once; 1: workgroup barrier (all waves read, then
 // all write); 2: a wave whose tiles averaged >= kHeavyLen bytes per frame waits until every wave of
 // the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
@@ -761,10 +929,13 @@ constexpr uint32_t kHeavyLen = 1024;
 // PF: load the descriptors of the wave's next tile while the current one streams.
 // WGT (tuning only): record each workgroup's start / end wall clock (100 MHz) after the counter
 // partials in the workspace (u64 [8192 + 2 g], [8192 + 2 g + 1]).
-template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false>
+// WIRE: the wire-format mode (a.opts != 0): 128-B windows (so TPW 1), wire_header_phase.
+template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
+    static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
+    constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
     const uint64_t wgt_start = WGT ? wall_clock64() : 0ull;
-    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kWin];  // 128 KiB at TPW 2
+    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kRowW];  // 128 KiB
     __shared__ __attribute__((aligned(16))) FrameMeta6 s_meta[kWaves6][kTile];          // 16 KiB
     __shared__ uint32_t s_sum[kWaves6][2][kTile];                                        // 8 KiB
     __shared__ uint32_t s_sort[STREAM >= 1 ? kWaves6 : 1][80];                          // 5 KiB (STREAM 1, 2)
@@ -824,16 +995,19 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             }
             const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
             const uint32_t len = dsc.z;
-            const uint64_t need = len >= 20 ? (len > 38 ? len : 38) : len;
+            // reference mode reads bytes [0, 38) whenever len >= 20 (xsk_receive.c:120-157); wire mode
+            // reads only [addr, addr + len) plus the window
+            const uint64_t need = WIRE ? len : (len >= 20 ? (len > 38 ? len : 38) : len);
             const bool ok = fi < a.n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
-            const bool parse = ok && len >= 20;
+            const bool parse = ok && len >= (WIRE ? 14u : 20u);
             const uint64_t a16 = addr & ~15ull;
             const uint32_t off = (uint32_t)addr & 15u;
             const uint32_t rowhi = parse ? off + len : 0u;
-            const uint32_t win = parse ? (uint32_t)min(a.umem_size - a16, (uint64_t)kWin) : 0u;
+            const uint32_t wend = ok ? (uint32_t)min(a.umem_size - a16, (uint64_t)kRowW) : 0u;
+            const uint32_t win = parse ? wend : 0u;
             const uint32_t lim = max(rowhi, win);
             const uint32_t nit = (lim + 255u) >> 8;
-            const bool short_tile = __ballot(lim > (uint32_t)kWin) == 0ull;
+            const bool short_tile = __ballot(lim > kRowW) == 0ull;
             uint64_t wlo = 0, span = ~0ull;
             if (!short_tile) {
                 wlo = wave_min_u64(nit ? a16 : ~0ull);
@@ -859,7 +1033,25 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                 WinLoader ld;
                 ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
                                                          fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
-                if (short_tile) {
+                if (WIRE && short_tile) {
+                    // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
+                    // nothing lies past byte 128, so the streamed part of every sum is zero
+                    const uint32_t kk = lane & 7u, ro = 16u * kk;
+                    u32x4 x[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
+                        const bool in = ro < fm.lim;
+                        x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? meta6_a16(fm) + ro : 0ull)));
+                    }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
+                        const u32x4 v = ro < meta[f].lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                        *(u32x4*)(rows + f * kRowW + ro) = v;
+                    }
+                    sums_ic[lane] = 0u;
+                } else if (short_tile) {
                     // every frame within its 64-B window: 4 lanes per frame, 16 frames per wave-load
                     const uint32_t kk = lane & 3u, ro = 16u * kk;
                     u32x4 x[4];
@@ -875,7 +1067,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         const FrameMeta6& fm = meta[f];
                         const uint32_t f_packed = fm.packed;
                         const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
-                        *(u32x4*)(rows + f * kWin + ro) = v;
+                        *(u32x4*)(rows + f * kRowW + ro) = v;
                         const int f_off = (int)(f_packed & 0xFFu), f_iphi = (int)((f_packed >> 8) & 0xFFu);
                         uint32_t rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
                         uint32_t ric = fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
@@ -891,13 +1083,14 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                 } else if (STREAM == 3 ||
                            (STREAM == 4 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                             uniform(max_nit_lane(nit)) < (uint32_t)U))) {
+                    static_assert(!WIRE || STREAM < 3, "wire mode uses the non-pipelined streams");
                     if (fast) stream_tile_sorted_pl<U, true>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                     else stream_tile_sorted_pl<U, false>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else if (STREAM == 1 ||
                            (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                             uniform(max_nit_lane(nit)) < (uint32_t)U))) {
-                    if (fast) stream_tile_sorted<U, true>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted<U, false>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    if (fast) stream_tile_sorted<U, true, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted<U, false, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else {
                     for (uint32_t s = 0; s < 16; ++s) {
                         const uint32_t f = 4u * s + q;
@@ -912,11 +1105,11 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         RowSums rs;
                         if (fast) {
                             ld.rel = fm.rel;
-                            stream_frame<U>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kWin, rs);
+                            stream_frame<U, WinLoader, WIRE>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                         } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
                             FarLoader fl;
                             fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
-                            stream_frame<U>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kWin, rs);
+                            stream_frame<U, FarLoader, WIRE>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                         }
                         const uint32_t ric = row_sum_dpp(fold64(rs.ic));
                         const uint32_t rip = row_sum_dpp(fold64(rs.ip));
@@ -933,8 +1126,13 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             __builtin_amdgcn_wave_barrier();
             const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
             const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
-            const bool wb = header_phase5<true, STREAM >= 1>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len,
-                                                             fi < a.n, ok, parse, fi, cnt, &rec[i], &verd[i]);
+            bool wb;
+            if (WIRE)
+                wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, fi < a.n, wend, cnt, &rec[i],
+                                       &verd[i]);
+            else
+                wb = header_phase5<true, STREAM >= 1>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, fi < a.n, ok,
+                                                       parse, fi, cnt, &rec[i], &verd[i]);
             wbm[i] = __ballot(wb);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();  // meta/sums are rewritten by the next tile
@@ -965,7 +1163,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                     const uint32_t fhi = (uint32_t)__shfl((int)ahi[i], (int)f, 64);
                     if ((wbm[i] >> f) & 1ull) {
                         const uint64_t fa = (uint64_t)flo | ((uint64_t)fhi << 32);
-                        *(u32x4*)(a.umem + fa + 16u * kk) = *(const u32x4*)(rows + f * kWin + 16u * kk);
+                        *(u32x4*)(a.umem + fa + 16u * kk) = *(const u32x4*)(rows + f * kRowW + 16u * kk);
                     }
                 }
             }

@@ -303,9 +303,20 @@ __global__ __launch_bounds__(NW * 64) void echo_wire_kernel(EchoArgs a, uint32_t
 
 }  // namespace
 
+// Implementation of the wire mode: 0 = the round kernel with WIRE (echo_kernel6<.., true>: one read of
+// every byte, the parse in the header phase; shipped), 1 = echo_wire_kernel (window first, then the
+// stream; kept for comparison).  Tuning switch only (xsk_gpu__set_wire_impl).
+static int g_wire_impl = 0;
+
 extern "C" {
 
 uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip
+
+int xsk_gpu__set_wire_impl(int impl) {
+    if (impl < 0 || impl > 1) return -EINVAL;
+    g_wire_impl = impl;
+    return 0;
+}
 
 // Internal: wire-mode launch (xsk_gpu_echo_dev_opts in xsk_echo.hip validates the arguments).
 int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
@@ -325,8 +336,13 @@ int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gp
     args.verdicts = d_verdicts;
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_partials;
-    echo_wire_kernel<kWireU, kWaves6, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, opts,
-                                                                                                   tiles_per_wg);
+    args.opts = opts;
+    if (g_wire_impl == 0)
+        echo_kernel6<kShip6U, 1, 2, 2, false, false, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(
+            args, tiles_per_wg);
+    else
+        echo_wire_kernel<kWireU, kWaves6, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, opts,
+                                                                                                       tiles_per_wg);
     HIP_TRY(hipGetLastError());
     *grid_out = grid;
     return 0;
