@@ -108,6 +108,7 @@ def test_wire_aligned_sector_path_and_window_edge():
 
 @pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED])
 def test_wire_host_umem_modes(mode):
+    _dev()
     umem, descs = mixed_batch(3000, 2048, seed=5, offsets=True)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, 7)
@@ -162,3 +163,30 @@ def test_wire_full_size_c3():
         v, r, _ = oracle.echo_batch_opts(frame, d1, X.OPT_ALL)
         assert v[0] == 0 and r[0] == recs[j]
         assert (got[k] == frame).all(), j
+
+
+def test_wire_multi_round_mixed():
+    """More tiles than one round of the persistent grid (270 K frames: several rounds per workgroup) of
+    random mixed traffic at odd and even offsets, every option on; also hits the STRICT re-read of a
+    message that ends before its frame and past the 128-B window."""
+    from tests.wire_frames import G, random_frame
+    _dev()
+    rng = np.random.default_rng(42)
+    pool = []
+    while len(pool) < 2048:
+        f, L = random_frame(rng)
+        pool.append((np.frombuffer(f, np.uint8), L))
+    # a few frames whose tot_len ends the message past the window but before the frame end
+    for _ in range(64):
+        f = G.build(payload=bytes(rng.integers(0, 256, 900, dtype=np.uint8)), tot_len=400, pad=0)
+        pool.append((np.frombuffer(f, np.uint8), len(f)))
+    n, stride = 270_000, 2048
+    umem = rng.integers(0, 256, n * stride + 256, dtype=np.uint8)
+    descs = np.zeros(n, oracle.DESC_DTYPE)
+    for i in range(n):
+        fr, L = pool[(i * 7919) % len(pool)]
+        a = i * stride + (i % 16)
+        umem[a:a + fr.size] = fr
+        descs[i] = (a, L, 0)
+    v = check(umem, descs, X.OPT_ALL)
+    assert (v == X.DROP_BAD_IP).any() and (v == 0).any()
