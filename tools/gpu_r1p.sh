@@ -4,6 +4,6 @@ mkdir -p $O
 run() { local name=$1 to=$2; shift 2
   echo "== $name $(date +%T)"; timeout -k 10 "$to" "$@" > "$O/$name.log" 2>&1; local rc=$?
   echo "rc=$rc"; tail -3 "$O/$name.log"; return $rc; }
-run wexpA 300 python tools/wexp.py 4096 30,31,32,33,34,35 256 || exit 1
-run wexpB 300 python tools/wexp.py 4096 0,31 4096 || exit 1
+run wexpA 300 python tools/wexp.py 4096 5,25,26,5,25,26 4096 || exit 1
+
 echo done

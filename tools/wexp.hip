@@ -29,6 +29,7 @@
 //   mode 19/20: mode 15/16 with two steps (8 frames, 12 loads per lane) in flight per wave
 //   mode 21/22: mode 15/16 with 1024-frame rounds (64 KiB LDS, two workgroups per CU: grid 512)
 //   mode 23/24: mode 21/22 with two steps in flight
+//   mode 25 / 26: write only, 48 / 32 B per frame (3 / 2 lanes x 16 B), no payload reads
 //   mode 30-35: read-only persistent layouts (grid = workgroups of 1024 threads, each a contiguous share
 //            of the frames): 30 = waves share a 64-frame chunk per step (= mode 16), 31 = every wave
 //            streams its own 64-frame tile (row q of step s: frame 4s+q), 32 = 31 with each workgroup
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
             } else if (MODE == 9) {
                 v[0] = k < 4 ? __builtin_nontemporal_load((const u32x4*)(fr + 16u * k)) : u32x4{0, 0, 0, 0};
                 acc += (uint64_t)v[0].x + v[0].y + v[0].z + v[0].w;
-            } else if (MODE != 5) {
+            } else if (MODE != 5 && MODE != 25 && MODE != 26) {
 #pragma unroll
                 for (int u = 0; u < 6; ++u) {
                     const uint32_t ro = 256u * u + 16u * k;
@@ -83,6 +84,8 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
                 v[0] = *(const u32x4*)(buf + 16u * k);  // same bytes for every frame: L2 hits
             }
             if ((MODE == 1 || MODE == 5 || MODE == 6) && k < 4) *(u32x4*)(fr + 16u * k) = v[0];
+            if (MODE == 25 && k < 3) *(u32x4*)(fr + 16u * k) = v[0];
+            if (MODE == 26 && k < 2) *(u32x4*)(fr + 16u * k) = v[0];
             if (MODE == 2 && k < 8) *(u32x4*)(fr + 16u * k) = v[0];
             if (MODE == 3) {
                 const uint32_t x0 = (uint32_t)__shfl((int)v[0].x, q * 16 + 0), x1 = (uint32_t)__shfl((int)v[0].y, q * 16 + 0),
@@ -275,6 +278,8 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 9: wexp_kernel<9><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 10: wexp_kernel<10><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 11: wexp_kernel<11><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
+        case 25: wexp_kernel<25><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
+        case 26: wexp_kernel<26><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;
         case 12: wexp_kernel<0><<<g, b, 0, s>>>(p, n, stride, len, o, side);
                  wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         case 15: wexp_rounds<true, false><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;

@@ -930,7 +930,10 @@ constexpr uint32_t kHeavyLen = 1024;
 // WGT (tuning only): record each workgroup's start / end wall clock (100 MHz) after the counter
 // partials in the workspace (u64 [8192 + 2 g], [8192 + 2 g + 1]).
 // WIRE: the wire-format mode (a.opts != 0): 128-B windows (so TPW 1), wire_header_phase.
-template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false>
+// NTS (tuning): write-phase stores nontemporal.  NOWR (tuning, wrong results): skip the write phase,
+// to time the read phase alone.
+template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
+          bool NTS = false, bool NOWR = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
@@ -1152,6 +1155,10 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const uint32_t t = r0 + (uint32_t)i * kWaves6 + wave;
+            if (NOWR) {  // keep the read phase alive without storing: fold the records into a counter
+                if (t < t_end) cnt.rxb += rec[i].x ^ rec[i].w ^ (uint32_t)wbm[i];
+                continue;
+            }
             if (t >= t_end) continue;
             const uint8_t* rows = s_hdr[wave][i];
             if (wbm[i]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
@@ -1163,13 +1170,18 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                     const uint32_t fhi = (uint32_t)__shfl((int)ahi[i], (int)f, 64);
                     if ((wbm[i] >> f) & 1ull) {
                         const uint64_t fa = (uint64_t)flo | ((uint64_t)fhi << 32);
-                        *(u32x4*)(a.umem + fa + 16u * kk) = *(const u32x4*)(rows + f * kRowW + 16u * kk);
+                        const u32x4 w = *(const u32x4*)(rows + f * kRowW + 16u * kk);
+                        if (NTS) __builtin_nontemporal_store(w, (u32x4*)(a.umem + fa + 16u * kk));
+                        else *(u32x4*)(a.umem + fa + 16u * kk) = w;
                     }
                 }
             }
             const uint32_t fi = t * kTile + lane;
             if (fi < a.n) {
-                if (a.recs) ((u32x4*)a.recs)[fi] = rec[i];
+                if (a.recs) {
+                    if (NTS) __builtin_nontemporal_store(rec[i], (u32x4*)a.recs + fi);
+                    else ((u32x4*)a.recs)[fi] = rec[i];
+                }
                 if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[i];
             }
         }
