@@ -43,6 +43,9 @@ extern "C" {
 /* Frames per wavefront tile == RX_BATCH_SIZE (src/lib/xsk_utils.h:8). */
 #define XSK_GPU_TILE_FRAMES 64
 
+/* Largest n one device-resident call accepts (frame indices stay 32-bit); larger n is -EINVAL. */
+#define XSK_GPU_MAX_BATCH 0xFFFFFF00u
+
 /* One RX descriptor. Binary-identical to `struct xdp_desc` of <linux/if_xdp.h>, which the reference
  * reads at src/lib/xsk_receive.c:222-223 (addr = UMEM offset, len = frame length). */
 struct xsk_gpu_desc {

@@ -103,6 +103,12 @@ def test_abi_version_and_argument_validation():
     assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2008, 1, None, None, None, None, None) == EINVAL
     assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2000, 1, None, 0x3008, None, None, None) == EINVAL
     assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2000, 1, None, None, 0x4000, None, None) == EINVAL  # stats w/o ws
+    assert L.xsk_gpu_echo_dev(0x1000, 4096, 0x2000, 0xFFFFFFFF, None, None, None, None, None) == EINVAL  # > MAX_BATCH
+    # wire-format options: unknown bits and the same argument checks
+    assert L.xsk_gpu_echo_dev_opts(0x1000, 4096, 0x2000, 1, 8, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev_opts(0x1001, 4096, 0x2000, 1, 7, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_echo_dev_opts(0x1000, 4096, 0x2000, 0xFFFFFFFF, 7, None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_set_options(None, 1) == EINVAL
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 8, 2048, 0, 0, 1, 0, 64, 64, None) == EINVAL
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 32, 0, 0, 1, 0, 64, 64, None) == EINVAL
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 2048, 0, 0, 1, 2, 64, 64, None) == EINVAL

@@ -189,6 +189,7 @@ int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_d
                       uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode, uint32_t len_lo,
                       uint32_t len_hi, void* stream) {
     if (n == 0) return 0;
+    if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
     if (!d_umem || !d_descs || (base_off & 15u) || (stride & 15u) || len_lo > len_hi || (mode != 0 && mode != 1) ||
         ((uintptr_t)d_umem & 15u))
         return -EINVAL;
@@ -225,6 +226,7 @@ int xsk_gpu_synth_dev(void* d_umem, uint64_t umem_size, struct xsk_gpu_desc* d_d
 int xsk_gpu_rearm_dev(void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts, uint32_t n,
                       void* stream) {
     if (n == 0) return 0;
+    if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
     if (!d_umem || !d_descs || !d_verdicts) return -EINVAL;
     hipLaunchKernelGGL(rearm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (uint8_t*)d_umem, d_descs,
                        d_verdicts, n);
@@ -235,6 +237,7 @@ int xsk_gpu_rearm_dev(void* d_umem, const struct xsk_gpu_desc* d_descs, const ui
 int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
                               uint32_t n, uint8_t* d_pack, uint32_t wire, void* stream) {
     if (n == 0) return 0;
+    if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
     hipLaunchKernelGGL(pack_headers_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t*)d_umem, d_descs, d_verdicts, n, d_pack, wire);
     HIP_TRY(hipGetLastError());

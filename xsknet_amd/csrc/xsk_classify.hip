@@ -111,7 +111,7 @@ int xsk_gpu_classify_dev(const void* d_umem, uint64_t umem_size, const struct xs
         return 0;
     }
     if (!d_umem || !d_descs || !d_actions || !d_workspace || (d_out && !d_nout) || ((uintptr_t)d_descs & 15u) ||
-        ((uintptr_t)d_out & 15u))
+        ((uintptr_t)d_out & 15u) || n > XSK_GPU_MAX_BATCH)
         return -EINVAL;
     const uint32_t nwg = (n + kCT - 1) / kCT;
     hipStream_t s = (hipStream_t)stream;

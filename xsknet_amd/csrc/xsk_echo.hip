@@ -104,6 +104,7 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                      void* d_workspace, void* stream) {
     if (n == 0) return 0;
+    if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
     if (!d_umem || !d_descs || ((uintptr_t)d_umem & 15u) || (umem_size & 15u) || ((uintptr_t)d_descs & 15u) ||
         ((uintptr_t)d_recs & 15u))
         return -EINVAL;
@@ -149,6 +150,7 @@ int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu
     if (opts == 0)
         return xsk_gpu_echo_dev(d_umem, umem_size, d_descs, n, d_verdicts, d_recs, d_stats, d_workspace, stream);
     if (n == 0) return 0;
+    if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
     if (!d_umem || !d_descs || ((uintptr_t)d_umem & 15u) || (umem_size & 15u) || ((uintptr_t)d_descs & 15u) ||
         ((uintptr_t)d_recs & 15u))
         return -EINVAL;

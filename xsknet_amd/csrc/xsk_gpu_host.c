@@ -95,7 +95,7 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
 
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
     int rc = 0;
-    if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || max_batch == 0 ||
+    if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || max_batch == 0 || max_batch > XSK_GPU_MAX_BATCH ||
         (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED))
         return -EINVAL;
     *out = NULL;
