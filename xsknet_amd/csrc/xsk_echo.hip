@@ -125,13 +125,17 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
     args.verdicts = d_verdicts;
     args.recs = d_recs;
     args.partials = d_stats ? (unsigned long long*)d_workspace : nullptr;
+    if (d_stats && grid == 1) {  // one workgroup: it adds its counters itself, no fold launch
+        args.partials = nullptr;
+        args.stats_direct = (unsigned long long*)&d_stats->rx_packets;
+    }
 
     const int slot = timer_slot(device);
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
     echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     HIP_TRY(hipGetLastError());
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], s));
-    if (d_stats) {
+    if (d_stats && grid > 1) {
         hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, s, (const unsigned long long*)d_workspace, grid,
                            d_stats);
         HIP_TRY(hipGetLastError());
@@ -141,7 +145,7 @@ int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc
 
 int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                            uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, void* d_partials,
-                           uint32_t* grid_out, void* stream);  // xsk_wire.hip
+                           struct xsk_gpu_stats* d_stats, uint32_t* grid_out, void* stream);  // xsk_wire.hip
 
 int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
@@ -161,10 +165,10 @@ int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu
     const int slot = timer_slot(device);
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], (hipStream_t)stream));
     const int rc = xsk_gpu__echo_wire_dev(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs,
-                                          d_stats ? d_workspace : nullptr, &grid, stream);
+                                          d_stats ? d_workspace : nullptr, d_stats, &grid, stream);
     if (rc) return rc;
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], (hipStream_t)stream));
-    if (d_stats) {
+    if (d_stats && grid > 1) {  // one workgroup added its counters itself
         hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
                            (const unsigned long long*)d_workspace, grid, d_stats);
         HIP_TRY(hipGetLastError());

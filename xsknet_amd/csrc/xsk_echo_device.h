@@ -31,6 +31,8 @@ struct EchoArgs {
     xsk_gpu_rec* recs;
     unsigned long long* partials;  // [gridDim.x][4]: rx_packets, rx_bytes, tx_packets, tx_bytes
     uint32_t opts = 0;             // XSK_GPU_OPT_* (wire-mode kernels only)
+    // one-workgroup launches: add the counters straight into the caller's stats (no fold launch)
+    unsigned long long* stats_direct = nullptr;  // &stats->rx_packets (4 consecutive u64)
 };
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -62,7 +64,7 @@ struct Counters {
 template <int NW = kWaves>
 __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, unsigned long long (*s_cnt)[4],
                                                uint32_t wave, uint32_t lane) {
-    if (!a.partials) return;
+    if (!a.partials && !a.stats_direct) return;
     c.rxp = wave_sum_u64(c.rxp);
     c.rxb = wave_sum_u64(c.rxb);
     c.txp = wave_sum_u64(c.txp);
@@ -78,7 +80,8 @@ __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, un
         unsigned long long s = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) s += s_cnt[w][threadIdx.x];
-        a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+        if (a.stats_direct) a.stats_direct[threadIdx.x] += s;  // gridDim.x == 1 (host guarantees)
+        else a.partials[blockIdx.x * 4 + threadIdx.x] = s;
     }
 }
 

@@ -8,7 +8,9 @@
  * per-frame loop would have, and returns per-frame verdicts plus the stats_record counters.
  *
  *   ZEROCOPY: the UMEM is registered as mapped pinned memory; the kernel reads and rewrites frames
- *             over PCIe in place.  One launch per batch; nothing but descriptors and results moves.
+ *             over PCIe in place, reads the descriptors from a mapped pinned staging buffer and writes
+ *             verdicts and counters straight into mapped pinned host memory: a batch is one kernel
+ *             launch (two when it spans more than one workgroup) and one synchronisation, no copies.
  *   STAGED:   frames are copied host->device into a device mirror of the UMEM (one strided 2-D copy
  *             when the chunk has a uniform frame stride, else the chunk's byte span), transformed in
  *             HBM, and only the 38 rewritten header bytes of TX_REPLY frames are copied back and
@@ -50,8 +52,12 @@ struct xsk_gpu_ctx {
     void* d_ws[NSTREAMS];
     uint8_t* d_pack;  /* STAGED: [max_batch][PACK] rewritten headers */
     uint8_t* h_pack;  /* STAGED: pinned host copy of d_pack */
-    uint8_t* h_verd;  /* pinned verdict staging */
-    struct xsk_gpu_stats* h_stats; /* [max_chunks] */
+    uint8_t* h_verd;  /* pinned (mapped) verdict staging */
+    struct xsk_gpu_stats* h_stats; /* [max_chunks], pinned (mapped) */
+    struct xsk_gpu_desc* h_descs;  /* ZEROCOPY: pinned (mapped) descriptor staging */
+    struct xsk_gpu_desc* m_descs;  /* ZEROCOPY: device aliases of h_descs / h_verd / h_stats */
+    uint8_t* m_verd;
+    struct xsk_gpu_stats* m_stats;
     hipStream_t stream[NSTREAMS];
     hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
     int registered;
@@ -83,6 +89,7 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (c->h_pack) (void)hipHostFree(c->h_pack);
     if (c->h_verd) (void)hipHostFree(c->h_verd);
     if (c->h_stats) (void)hipHostFree(c->h_stats);
+    if (c->h_descs) (void)hipHostFree(c->h_descs);
     if (c->done) {
         for (uint32_t i = 0; i < c->max_chunks; i++)
             if (c->done[i]) (void)hipEventDestroy(c->done[i]);
@@ -95,8 +102,8 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
 
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
     int rc = 0;
-    if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || max_batch == 0 || max_batch > XSK_GPU_MAX_BATCH ||
-        (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED))
+    if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || max_batch == 0 ||
+        max_batch > XSK_GPU_MAX_BATCH || (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED))
         return -EINVAL;
     *out = NULL;
     int ndev = 0;
@@ -133,8 +140,14 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
         }
         for (int s = 0; s < NSTREAMS; s++) TRY(hipMalloc(&c->d_ws[s], ws));
     }
-    TRY(hipHostMalloc((void**)&c->h_verd, max_batch, hipHostMallocDefault));
-    TRY(hipHostMalloc((void**)&c->h_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats), hipHostMallocDefault));
+    TRY(hipHostMalloc((void**)&c->h_verd, max_batch, hipHostMallocMapped));
+    TRY(hipHostMalloc((void**)&c->h_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats), hipHostMallocMapped));
+    if (mode == XSK_GPU_MODE_ZEROCOPY) {
+        TRY(hipHostMalloc((void**)&c->h_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc), hipHostMallocMapped));
+        TRY(hipHostGetDevicePointer((void**)&c->m_descs, c->h_descs, 0));
+        TRY(hipHostGetDevicePointer((void**)&c->m_verd, c->h_verd, 0));
+        TRY(hipHostGetDevicePointer((void**)&c->m_stats, c->h_stats, 0));
+    }
     c->done = (hipEvent_t*)calloc(c->max_chunks, sizeof(hipEvent_t));
     if (!c->done) {
         rc = -ENOMEM;
@@ -200,6 +213,15 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
                          int want_recs, int s) {
     int rc = 0;
     const hipStream_t st = c->stream[s];
+    if (c->mode == XSK_GPU_MODE_ZEROCOPY) { /* descriptors in, verdicts and counters out: mapped host memory */
+        memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
+        memset(&c->h_stats[ci], 0, sizeof c->h_stats[ci]);
+        rc = xsk_gpu_echo_dev_opts(c->d_umem, c->umem_size, c->m_descs + i0, n, c->opts, c->m_verd + i0,
+                                   want_recs ? c->d_recs + i0 : NULL, c->m_stats + ci, c->d_ws[s], st);
+        if (rc) goto out;
+        TRY(hipEventRecord(c->done[ci], st));
+        return 0;
+    }
     struct xsk_gpu_desc* dd = c->d_descs + i0;
     TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, st));
     TRY(hipMemsetAsync(c->d_stats + ci, 0, sizeof(struct xsk_gpu_stats), st));
