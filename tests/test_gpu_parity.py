@@ -499,14 +499,16 @@ def test_more_tiles_than_grid():
     assert torch.equal(before, d_umem)
 
 
-def test_tile_spanning_more_than_2gib():
-    """Frames of one tile more than 2 GiB apart (the kernel's 64-bit-address path)."""
+@pytest.mark.parametrize("mode,lo,hi,opts", [(1, 20, 1500, 0), (0, 1500, 1500, 0), (1, 20, 1500, 7), (0, 1500, 1500, 7)])
+def test_tile_spanning_more_than_2gib(mode, lo, hi, opts):
+    """Frames of one tile more than 2 GiB apart (the kernel's 64-bit-address path): ragged tiles take the
+    sorted streams, uniform 1500-B tiles the per-step streams; reference and wire mode."""
     dev = _dev()
     size = (2 << 30) + (512 << 20)  # 2.5 GiB UMEM
     far = (2 << 30) + (64 << 20)
     n = 200
     tmp = np.zeros(n * 2048, np.uint8)
-    src = oracle.synth_batch(tmp, n, 0, 2048, seed=0x5EED1212, mode=1, len_lo=20, len_hi=1500)
+    src = oracle.synth_batch(tmp, n, 0, 2048, seed=0x5EED1212, mode=mode, len_lo=lo, len_hi=hi)
     d_umem = torch.zeros(size, dtype=torch.uint8, device=dev)
     descs = np.zeros(n, X.DESC_DTYPE)
     for i in range(n):
@@ -518,7 +520,7 @@ def test_tile_spanning_more_than_2gib():
     hi_before = d_umem[far:far + n * 2048 + 64].cpu().numpy().copy()
     verd = torch.zeros(n, dtype=torch.uint8, device=dev)
     recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    X.echo_dev(d_umem, d_descs, n, verd, recs)
+    X.echo_dev(d_umem, d_descs, n, verd, recs, opts=opts)
     torch.cuda.synchronize()
     # oracle on a compact host image: both regions, same relative layout
     img = np.zeros(2 * (n * 2048 + 64), np.uint8)
@@ -526,7 +528,7 @@ def test_tile_spanning_more_than_2gib():
     img[n * 2048 + 64:] = hi_before
     hd = descs.copy()
     hd["addr"] = np.where(np.arange(n) % 2 == 1, descs["addr"] - far + n * 2048 + 64, descs["addr"])
-    v_ref, r_ref, _ = oracle.echo_batch(img, hd)
+    v_ref, r_ref, _ = oracle.echo_batch_opts(img, hd, opts)
     assert (verd.cpu().numpy() == v_ref).all()
     assert (recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
     assert (d_umem[:n * 2048 + 64].cpu().numpy() == img[:n * 2048 + 64]).all()
