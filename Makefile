@@ -11,7 +11,7 @@ LIB      := xsknet_amd/libxsknet_amd.so
 
 all: $(LIB) oracle tools/echo_replay
 
-DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
+DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_variants.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
 HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_tune.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_wire.o
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)

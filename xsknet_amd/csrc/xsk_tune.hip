@@ -11,6 +11,7 @@
 #include <errno.h>
 
 #include "xsk_echo_device.h"
+#include "xsk_echo_variants.h"
 #include "xsk_hip_util.h"
 
 using namespace xskgpu;
