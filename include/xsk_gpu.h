@@ -153,11 +153,12 @@ size_t xsk_gpu_workspace_size(int device, uint32_t n);
  *   d_descs          : n descriptors (device memory, 16-B aligned)
  *   d_verdicts       : n bytes, or NULL
  *   d_recs           : n records (16-B aligned), or NULL
- *   d_stats          : one xsk_gpu_stats in device memory, accumulated; or NULL
+ *   d_stats          : one xsk_gpu_stats in device memory (not mapped host memory: every workgroup adds
+ *                      its counters with device-scope atomics), accumulated; or NULL
  *   d_workspace      : xsk_gpu_workspace_size() bytes of device memory; may be NULL iff d_stats is
  *   stream           : hipStream_t (NULL = default stream)
- * Asynchronous: enqueues the transform kernel (and, with d_stats, a one-workgroup counter fold) on
- * `stream` and returns.  Replaces xsk_receive.c:220-233 for one batch. */
+ * Asynchronous: enqueues the transform kernel on `stream` and returns.  Replaces xsk_receive.c:220-233
+ * for one batch. */
 int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                      void* d_workspace, void* stream);

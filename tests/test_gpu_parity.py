@@ -210,6 +210,38 @@ def test_stats_accumulate_across_calls():
     assert (d_umem.cpu().numpy() == ref).all()
 
 
+@pytest.mark.parametrize("atomic", [1, 0])
+def test_counter_delivery_modes(atomic):
+    """Both counter deliveries (device atomics, shipped; partials + fold launch) accumulate the oracle's
+    counters over many workgroups, on top of what the stats already hold, and leave `timestamp` alone."""
+    import ctypes as C
+    dev = _dev()
+    L = X.lib()
+    L.xsk_gpu__set_stats_atomic.argtypes = [C.c_int]
+    n = 300_000  # tiles for every workgroup of a 256-CU grid, plus a ragged tail
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=77, mode=1, len_lo=0, len_hi=1500)
+    ref = umem.copy()
+    _, _, s_ref = oracle.echo_batch(ref, descs)
+    d_umem, d_descs = to_dev(umem), to_dev(descs)
+    base = np.zeros(1, X.STATS_DTYPE)
+    base["timestamp"], base["rx_packets"], base["rx_bytes"] = 0x1234, 5, 1 << 40
+    base["tx_packets"], base["tx_bytes"] = 7, 11
+    d_stats = to_dev(base)
+    ws = torch.zeros(X.workspace_size(0, n), dtype=torch.uint8, device=dev)
+    assert L.xsk_gpu__set_stats_atomic(atomic) == 0
+    try:
+        X.echo_dev(d_umem, d_descs, n, None, None, d_stats, ws)
+        torch.cuda.synchronize()
+    finally:
+        L.xsk_gpu__set_stats_atomic(1)
+    s = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        assert int(s[k]) == int(s_ref[k]) + int(base[k][0]), k
+    assert int(s["timestamp"]) == 0x1234
+    assert (d_umem.cpu().numpy() == ref).all()
+
+
 @pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED])
 def test_host_umem_modes(mode):
     """C1 shape: 4096 frames in a 16 MiB UMEM of 4 KiB chunks, RX batches of 64 (and one big batch)."""

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Driver for tools/glds.hip (register loads vs LDS-DMA read ceiling, GPU box)."""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "libglds.so")
+if not os.path.exists(SO):
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", SO,
+                    os.path.join(HERE, "glds.hip")], check=True)
+L = C.CDLL(SO)
+L.glds_run.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                       C.c_void_p]
+
+NAMES = {0: "reg U4", 1: "reg U8", 2: "glds U4 nt", 3: "glds U8 nt", 4: "glds U4 default", 5: "glds U8 default",
+         6: "glds U16 nt"}
+
+
+def main():
+    dev = torch.device("cuda:0")
+    n, stride, ln = 1 << 20, 4096, 1500
+    slabs = [torch.randint(0, 255, (n * stride,), dtype=torch.uint8, device=dev) for _ in range(2)]
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+    rows = (ln + 255) // 256
+    cases = [("contig_1.5GB", 0, n * ln // 1024), ("c3_rows_s4096", 1, n // 4 * rows)]
+    res = {}
+    for rep in range(8):
+        for cname, layout, npieces in cases:
+            for kind in NAMES:
+                for grid in (1024, 2048):
+                    for s in slabs:
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        assert L.glds_run(kind, s.data_ptr(), npieces, layout, ln, stride, grid, out.data_ptr(), sp) == 0
+                        e1.record()
+                        if rep:
+                            res.setdefault((cname, kind, grid), []).append((e0, e1))
+        torch.cuda.synchronize()
+    for (cname, kind, grid), evs in res.items():
+        ts = sorted(a.elapsed_time(b) for a, b in evs)
+        med = ts[len(ts) // 2] * 1e3
+        print(json.dumps({"case": cname, "kind": NAMES[kind], "grid": grid, "us_med": round(med, 1),
+                          "us_min": round(ts[0] * 1e3, 1), "tbs_frame_bytes": round(n * ln / med / 1e6, 3)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

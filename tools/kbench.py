@@ -30,6 +30,7 @@ LAYOUTS = {
     "c3_s1504": (1 << 20, 1500, 1500, 1504),
     "c2_s64": (1 << 20, 64, 64, 64),
     "c4_s2048": (1 << 20, 64, 1500, 2048),
+    "c4ramp_s2048": (1 << 20, 1500, 1500, 2048),  # lengths overwritten: 64..1500 ramp, the same in every tile
     "p98_s2048": (1 << 20, 98, 98, 2048),      # a default ping (56-B payload) per frame
     "m512_s2048": (1 << 20, 64, 512, 2048),
 }
@@ -59,6 +60,9 @@ def main():
             u = torch.empty(n * stride, dtype=torch.uint8, device=dev)
             d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
             X.synth_dev(u, d, n, 0, stride, 0x5EED0003, b * n, 1, 0, lo, hi)
+            if lname.startswith("c4ramp"):  # equal bytes per tile, ragged inside (mean 782 B)
+                ramp = 64 + (torch.arange(n, device=dev) % 64) * 1436 // 63
+                d.view(torch.int32).view(-1, 4)[:, 2] = ramp.to(torch.int32)
             umems.append(u)
             descss.append(d)
         nbytes = int(descss[0].view(torch.int32).view(-1, 4)[:, 2].to(torch.int64).sum().item())

@@ -80,7 +80,9 @@ __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, un
         unsigned long long s = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) s += s_cnt[w][threadIdx.x];
-        if (a.stats_direct) a.stats_direct[threadIdx.x] += s;  // gridDim.x == 1 (host guarantees)
+        if (a.stats_direct && gridDim.x == 1) a.stats_direct[threadIdx.x] += s;
+        else if (a.stats_direct)  // every workgroup adds its own: non-returning device-scope atomics
+            __hip_atomic_fetch_add(a.stats_direct + threadIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else a.partials[blockIdx.x * 4 + threadIdx.x] = s;
     }
 }

@@ -30,6 +30,10 @@
 
 int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
                               uint32_t n, uint8_t* d_pack, uint32_t wire, void* stream);
+/* xsk_gpu_echo_dev_opts for counters in mapped host memory (always the fold launch, no device atomics) */
+int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                                     uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
+                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream);
 
 #define NSTREAMS 2
 #define CHUNK_FRAMES 32768u /* staged pipeline granule: ~49 MB of 1500-B frames per copy-in */
@@ -216,7 +220,7 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
     if (c->mode == XSK_GPU_MODE_ZEROCOPY) { /* descriptors in, verdicts and counters out: mapped host memory */
         memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
         memset(&c->h_stats[ci], 0, sizeof c->h_stats[ci]);
-        rc = xsk_gpu_echo_dev_opts(c->d_umem, c->umem_size, c->m_descs + i0, n, c->opts, c->m_verd + i0,
+        rc = xsk_gpu__echo_dev_opts_hoststats(c->d_umem, c->umem_size, c->m_descs + i0, n, c->opts, c->m_verd + i0,
                                    want_recs ? c->d_recs + i0 : NULL, c->m_stats + ci, c->d_ws[s], st);
         if (rc) goto out;
         TRY(hipEventRecord(c->done[ci], st));

@@ -321,7 +321,7 @@ int xsk_gpu__set_wire_impl(int impl) {
 // Internal: wire-mode launch (xsk_gpu_echo_dev_opts in xsk_echo.hip validates the arguments).
 int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                            uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, void* d_partials,
-                           struct xsk_gpu_stats* d_stats, uint32_t* grid_out, void* stream) {
+                           struct xsk_gpu_stats* d_stats, int fold, uint32_t* grid_out, void* stream) {
     int device = 0;
     HIP_TRY(hipGetDevice(&device));
     const uint32_t ncu = xsk_gpu__num_cu(device);
@@ -337,7 +337,7 @@ int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gp
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_partials;
     args.opts = opts;
-    if (d_stats && grid == 1) {  // one workgroup: it adds its counters itself, no fold launch
+    if (d_stats && (grid == 1 || !fold)) {  // the workgroups add their counters themselves (no fold launch)
         args.partials = nullptr;
         args.stats_direct = (unsigned long long*)&d_stats->rx_packets;
     }
