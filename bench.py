@@ -5,7 +5,7 @@ One step = one pass of the transform (xsk_gpu_echo_dev: parse + full-payload che
 rewrite + records + stats counters) over one batch of frames already resident in HBM.  Each step
 gets a fresh, never-transformed batch (a pool of pre-generated batches), so no step sees replies.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4] [--no-cpu] [--host-inclusive]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5|p98] [--no-cpu] [--host-inclusive]
 
 Multi-GPU: one process per GPU (torch.distributed.run); frame i of a step's global batch goes to
 GPU i mod N (round-robin sharding, no data-path collective); per-GPU work is fixed -> weak scaling.
@@ -25,7 +25,7 @@ import torch  # noqa: E402
 
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false>"  # the transform kernel xsk_gpu_echo_dev launches
+KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true>"  # the transform kernel xsk_gpu_echo_dev launches
 WIRE_KERNEL = "echo_kernel6<4, 1, 2, 2, false, false, true, false, false>"  # xsk_gpu_echo_dev_opts, nonzero --opts
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
@@ -33,6 +33,8 @@ CONFIGS = {
     "c3": (1 << 20, 1500, 1500, 4096, 0x5EED0003,
            "c3: 1M x 1500B ICMP echo frames, 4 KiB UMEM-chunk stride, full-payload checksum"),
     "c4": (1 << 20, 64, 1500, 2048, 0x5EED0004, "c4: 1M x U{64..1500}B ICMP echo frames, 2 KiB stride"),
+    # not a BASELINE config: the frame a default `ping` sends (56-B payload), for the RX-loop case
+    "p98": (1 << 20, 98, 98, 2048, 0x5EED0098, "p98: 1M x 98B default-ping ICMP echo frames, 2 KiB stride"),
     # C5 is a STRONG-scaling config: 64 M frames in total per step, frame i on GPU i mod N
     "c5": (1 << 26, 1500, 1500, 2048, 0x5EED0005,
            "c5: 64M x 1500B ICMP echo frames per step in total, round-robin over the GPUs, 2 KiB stride"),

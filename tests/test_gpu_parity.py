@@ -114,7 +114,8 @@ def test_mixed_parity(n):
     check_against_oracle(umem, descs)
 
 
-@pytest.mark.parametrize("stride,lo,hi", [(64, 64, 64), (1536, 1500, 1500), (4096, 1500, 1500), (4096, 64, 4032)])
+@pytest.mark.parametrize("stride,lo,hi", [(64, 64, 64), (1536, 1500, 1500), (4096, 1500, 1500), (4096, 64, 4032),
+                                           (2048, 98, 98), (2048, 42, 128), (128, 98, 128)])
 def test_valid_parity_layouts(stride, lo, hi):
     n = 5000
     umem = np.zeros(n * stride, np.uint8)
@@ -369,10 +370,12 @@ def test_timing_hook():
     assert cnt == 3 and ms > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87])
 @pytest.mark.parametrize("grid", [0, 1, 7])
-def test_kernel_variants_parity(variant, grid):
-    """Every ring depth / grid shape the tuning sweep may select is bit-exact (multi-tile waves too)."""
+@pytest.mark.parametrize("len_hi", [2048, 112])
+def test_kernel_variants_parity(variant, grid, len_hi):
+    """Every ring depth / grid shape the tuning sweep may select is bit-exact (multi-tile waves too);
+    len_hi 112 makes tiles of ping-size frames (every frame within 128 B of its 16-B aligned start)."""
     import ctypes as C
     L = X.lib()
     L.xsk_gpu__echo_variant.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
@@ -380,7 +383,7 @@ def test_kernel_variants_parity(variant, grid):
     dev = _dev()
     n, stride = 3000, 2048 + 16
     umem = np.zeros(n * stride + 64, np.uint8)
-    descs = oracle.synth_batch(umem, n, 0, stride, seed=0x5EED0707, mode=1, len_lo=20, len_hi=2048)
+    descs = oracle.synth_batch(umem, n, 0, stride, seed=0x5EED0707, mode=1, len_lo=20, len_hi=len_hi)
     descs["addr"] += (np.arange(n) % 7).astype(np.uint64)  # shift frames: odd / unaligned starts
     for j in range(n - 1, -1, -1):  # move the bytes accordingly (back to front)
         a = j * stride

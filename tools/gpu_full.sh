@@ -12,6 +12,7 @@ run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
 run bench_c3 400 python bench.py --steps 20 --warmup 3 || exit 1
 run bench_c4 300 python bench.py --config c4 --steps 20 --warmup 3 --no-cpu || exit 1
 run bench_c2 300 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu || exit 1
+run bench_p98 300 python bench.py --config p98 --steps 20 --warmup 3 --no-cpu || exit 1
 run bench_c3_wire 300 python bench.py --opts 7 --steps 20 --warmup 3 --no-cpu || exit 1
 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --no-cpu || exit 1
 run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc_fetch -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 4 --warmup 1 --no-cpu || exit 1

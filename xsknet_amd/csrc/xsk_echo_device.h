@@ -359,6 +359,7 @@ constexpr int kShip6U = 4;                  // row-loads in flight per lane
 constexpr int kShip6TPW = 2;                // tiles per wave per round: 2048 frames per CU per round
 constexpr int kShip6Sync = 2;               // heavy waves wait for the round, light ones go ahead
 constexpr int kShip6Stream = 2;             // per-step streams for uniform long tiles, sorted step-packed otherwise
+constexpr bool kShip6Mid = true;            // ping-size tiles (every frame within 128 B): 8 loads at once
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -777,7 +778,7 @@ constexpr uint32_t kHeavyLen = 1024;
 // NTS (tuning): write-phase stores nontemporal.  NOWR (tuning, wrong results): skip the write phase,
 // to time the read phase alone.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false>
+          bool NTS = false, bool NOWR = false, bool MID = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
@@ -855,12 +856,13 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             const uint32_t lim = max(rowhi, win);
             const uint32_t nit = (lim + 255u) >> 8;
             const bool short_tile = __ballot(lim > kRowW) == 0ull;
+            const bool mid_tile = MID && !WIRE && !short_tile && __ballot(lim > 128u) == 0ull;
             uint64_t wlo = 0, span = ~0ull;
             if (!short_tile) {
                 wlo = wave_min_u64(nit ? a16 : ~0ull);
                 span = wave_max_u64(nit ? a16 + lim : 0ull) - wlo;
             }
-            const bool fast = !short_tile && span < 0x80000000ull;  // wave-uniform
+            const bool fast = !short_tile && !mid_tile && span < 0x80000000ull;  // wave-uniform
             {
                 FrameMeta6 m;
                 m.rel = fast ? (nit ? (uint32_t)(a16 - wlo) : 0u) : (uint32_t)(a16 >> 4);
@@ -926,6 +928,30 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                             sums_ic[f] = ric;
                             sums_ip[f] = rip;
                         }
+                    }
+                } else if (MID && !WIRE && mid_tile) {
+                    // every frame within 128 B of its 16-B aligned start (pings): 8 lanes per frame, 8 frames
+                    // per wave-load, all 8 loads in flight at once; the ICMP sum by exact byte range, reduced
+                    // over the 8 lanes (the IPv4 header sum comes from the window in the header phase)
+                    const uint32_t kk = lane & 7u, ro = 16u * kk;
+                    u32x4 x[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
+                        const bool in = ro < fm.lim;
+                        x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? meta6_a16(fm) + ro : 0ull)));
+                    }
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
+                        const FrameMeta6& fm = meta[f];
+                        const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                        if (kk < 4u) *(u32x4*)(rows + f * kRowW + ro) = v;
+                        uint32_t ric = fold64(sum_range(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi));
+                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);   // xor 1
+                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);   // xor 2
+                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x141, 0xF, 0xF, false);  // half-row mirror
+                        if (kk == 0u) sums_ic[f] = ric;
                     }
                 } else if (STREAM == 3 ||
                            (STREAM == 4 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||

@@ -375,6 +375,8 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 80: echo_kernel6<4, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 84: echo_kernel6<4, 2, 2, 2, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
             case 85: echo_kernel6<4, 2, 2, 2, false, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 86: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 87: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
