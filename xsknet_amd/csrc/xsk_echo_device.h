@@ -146,6 +146,16 @@ struct RowSums {
 __device__ __forceinline__ uint64_t sum_dw(u32x4 x) {
     return (uint64_t)x.x + (uint64_t)x.y + (uint64_t)x.z + (uint64_t)x.w;
 }
+// acc + the eight 16-bit halves of x: one v_dot2_u32_u16 per dword (against 1,1) instead of a 64-bit add
+// pair.  Sum of halves == sum of dwords mod 0xFFFF and both are zero only for all-zero data, so the folded
+// RFC 1071 result is the same; callers flush acc into their 64-bit sum every few blocks (no overflow).
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2_halves(uint32_t v, uint32_t acc) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2_t, v), u16x2_t{1, 1}, acc, false);
+}
+__device__ __forceinline__ uint32_t sum_halves(u32x4 x, uint32_t acc) {
+    return dot2_halves(x.w, dot2_halves(x.z, dot2_halves(x.y, dot2_halves(x.x, acc))));
+}
 // sum of the bytes of block x (row bytes [ro, ro+16)) that lie in [lo, hi)
 __device__ __forceinline__ uint64_t sum_range(u32x4 x, int ro, int lo, int hi) {
     return (uint64_t)keep_bytes(x.x, ro, lo, hi) + (uint64_t)keep_bytes(x.y, ro + 4, lo, hi) +
@@ -170,7 +180,7 @@ struct FrameMeta {
 // WIRE (wire-format mode): the window is 128 B (lanes 0-7) and the stream sums only row bytes
 // [128, rowhi) -- the parse, and so the ICMP start and end, are known only in the header phase, which
 // sums the in-window part from LDS (wire_header_phase).
-template <int U, class L, bool WIRE = false>
+template <int U, class L, bool WIRE = false, bool D2 = false>
 __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t f_rowhi, uint32_t f_lim,
                                              uint32_t f_off, uint32_t f_iphi, uint32_t k, uint8_t* hdr_row,
                                              RowSums& rs) {
@@ -185,6 +195,7 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
     }
     for (uint32_t j0 = 0; j0 < ns; j0 += U) {
         u32x4 v[U];
+        uint32_t h = 0;  // D2: halves of this batch's blocks
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
@@ -206,12 +217,16 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
                     y.y &= dw_mask(nb - 4);
                     y.z &= dw_mask(nb - 8);
                     y.w &= dw_mask(nb - 12);
-                    rs.ic += sum_dw(y);
+                    if (D2) h = sum_halves(y, h);
+                    else rs.ic += sum_dw(y);
+                } else if (D2) {
+                    h = sum_halves(x, h);
                 } else {
                     rs.ic += sum_dw(x);  // whole block in the frame, or zeros past it
                 }
             }
         }
+        if (D2) rs.ic += h;
     }
 }
 
@@ -379,7 +394,7 @@ __device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
 // (ragged batches waste fewer lanes), and each batch of U row-loads is packed across consecutive steps
 // by a wave-uniform cursor (short frames share one round trip instead of paying one per step).  The
 // IPv4 header sum is taken in the header phase from the LDS window (header_phase5<.., IPH = true>).
-template <int U, bool FAST, bool WIRE = false>
+template <int U, bool FAST, bool WIRE = false, bool D2 = false>
 __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
                                                    const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
                                                    uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
@@ -443,17 +458,19 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
                 }
             }
         }
+        uint32_t h = 0;  // D2: halves of this batch's blocks of step `cur`
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (us[u] >= 16u) continue;  // uniform
             if (us[u] != cur) {          // uniform: a new step begins in this slot
                 if (cur < 16u) {
-                    const uint32_t r = row_sum_dpp(fold64(ic));
+                    const uint32_t r = row_sum_dpp(fold64(ic + h));
                     if (k == 15u) sums_ic[cur_f] = r;
                 }
                 cur = us[u];
                 cur_f = uf[u];
                 ic = 0;
+                h = 0;
             }
             const uint32_t ro = 256u * uj[u] + 16u * k;
             const u32x4 x = v[u];
@@ -467,9 +484,11 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
                 y.y &= dw_mask(nb - 4);
                 y.z &= dw_mask(nb - 8);
                 y.w &= dw_mask(nb - 12);
-                ic += sum_dw(y);
+                if (D2) h = sum_halves(y, h);
+                else ic += sum_dw(y);
             }
         }
+        if (D2) ic += h;
     }
     if (cur < 16u) {
         const uint32_t r = row_sum_dpp(fold64(ic));
@@ -778,7 +797,7 @@ constexpr uint32_t kHeavyLen = 1024;
 // NTS (tuning): write-phase stores nontemporal.  NOWR (tuning, wrong results): skip the write phase,
 // to time the read phase alone.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false, bool MID = false>
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
@@ -811,7 +830,12 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         if (t_begin + wave < t_end && f0 < a.n) dnext = *(const u32x4*)(a.descs + f0);
     }
 
-    for (uint32_t r0 = t_begin; r0 < t_end; r0 += kRound) {  // workgroup-uniform
+    // SYNC 3/4 (tuning only): chip-wide barriers around every write phase, on a counter the host zeroes
+    // before the launch (u32 at partials + 64 Ki); every workgroup runs the same number of rounds.
+    uint32_t* gbar = (SYNC >= 3 && a.partials) ? (uint32_t*)(a.partials + 65536) : nullptr;
+    uint32_t gbar_n = 0;
+    const uint32_t r_end = SYNC >= 3 ? t_begin + tiles_per_wg : t_end;
+    for (uint32_t r0 = t_begin; r0 < r_end; r0 += kRound) {  // workgroup-uniform
         u32x4 rec[TPW];
         uint32_t verd[TPW], alo[TPW], ahi[TPW];
         uint64_t wbm[TPW];
@@ -962,8 +986,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                 } else if (STREAM == 1 ||
                            (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                             uniform(max_nit_lane(nit)) < (uint32_t)U))) {
-                    if (fast) stream_tile_sorted<U, true, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted<U, false, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    if (fast) stream_tile_sorted<U, true, WIRE, D2>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted<U, false, WIRE, D2>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else {
                     for (uint32_t s = 0; s < 16; ++s) {
                         const uint32_t f = 4u * s + q;
@@ -978,11 +1002,11 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         RowSums rs;
                         if (fast) {
                             ld.rel = fm.rel;
-                            stream_frame<U, WinLoader, WIRE>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                            stream_frame<U, WinLoader, WIRE, D2>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                         } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
                             FarLoader fl;
                             fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
-                            stream_frame<U, FarLoader, WIRE>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                            stream_frame<U, FarLoader, WIRE, D2>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                         }
                         const uint32_t ric = row_sum_dpp(fold64(rs.ic));
                         const uint32_t rip = row_sum_dpp(fold64(rs.ip));
@@ -1013,6 +1037,18 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
 
         // ================= write phase: every wave of the workgroup has finished reading =================
         if (SYNC == 1) __syncthreads();
+        if (SYNC >= 3 && gbar) {  // every workgroup of the chip has finished reading this round
+            __syncthreads();
+            ++gbar_n;
+            if (threadIdx.x == 0) {
+                __hip_atomic_fetch_add(gbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // bounded spin (~0.1 s): a workgroup that is not resident can delay, never hang, the launch
+                for (uint32_t it = 0; it < (1u << 21) &&
+                     __hip_atomic_load(gbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gbar_n * gridDim.x; ++it)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            __syncthreads();
+        }
         if (SYNC == 2) {
             ++rounds_done;
             if (lane == 0) atomicAdd(&s_arrive, 1u);
@@ -1057,6 +1093,19 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next round
+        if (SYNC == 4 && gbar) {  // ... and every workgroup has issued its writes before anyone reads on
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            ++gbar_n;
+            if (threadIdx.x == 0) {
+                __hip_atomic_fetch_add(gbar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // bounded spin (~0.1 s): a workgroup that is not resident can delay, never hang, the launch
+                for (uint32_t it = 0; it < (1u << 21) &&
+                     __hip_atomic_load(gbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gbar_n * gridDim.x; ++it)
+                    __builtin_amdgcn_s_sleep(1);
+            }
+            __syncthreads();
+        }
     }
     store_partials<kWaves6>(a, cnt, s_cnt, wave, lane);
     if (WGT && threadIdx.x == 0 && a.partials) {

@@ -345,12 +345,16 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_workspace;
     hipStream_t s = (hipStream_t)stream;
-    if (variant >= 60 && variant < 90) {  // round kernel: max_grid = workgroups (0: one per CU)
+    if (variant >= 60 && variant < 100) {  // round kernel: max_grid = workgroups (0: one per CU)
         int device = 0;
         HIP_TRY(hipGetDevice(&device));
         uint32_t g6 = 0, per = 0;
         echo6_geometry(n, max_grid ? max_grid : xsk_gpu__num_cu(device), &g6, &per);
         const dim3 gg(g6), bb(kThreads6);
+        if (variant == 90 || variant == 91) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
+            if (!d_workspace) return -EINVAL;
+            HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
+        }
         switch (variant) {
             case 60: echo_kernel6<4, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 61: echo_kernel6<6, 2><<<gg, bb, 0, s>>>(args, per); break;
@@ -377,6 +381,10 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 85: echo_kernel6<4, 2, 2, 2, false, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
             case 86: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
             case 87: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 88: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 89: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 90: echo_kernel6<4, 2, 3, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 91: echo_kernel6<4, 2, 4, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
