@@ -372,10 +372,11 @@ def test_timing_hook():
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88])
 @pytest.mark.parametrize("grid", [0, 1, 7])
-@pytest.mark.parametrize("len_hi", [2048, 112])
+@pytest.mark.parametrize("len_hi", [2048, 112, 48])
 def test_kernel_variants_parity(variant, grid, len_hi):
     """Every ring depth / grid shape the tuning sweep may select is bit-exact (multi-tile waves too);
-    len_hi 112 makes tiles of ping-size frames (every frame within 128 B of its 16-B aligned start)."""
+    len_hi 112 makes tiles of ping-size frames (every frame within 128 B of its 16-B aligned start), 48
+    tiles whose frames all fit their 64-B windows."""
     import ctypes as C
     L = X.lib()
     L.xsk_gpu__echo_variant.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,

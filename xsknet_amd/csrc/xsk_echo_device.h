@@ -156,6 +156,13 @@ __device__ __forceinline__ uint32_t dot2_halves(uint32_t v, uint32_t acc) {
 __device__ __forceinline__ uint32_t sum_halves(u32x4 x, uint32_t acc) {
     return dot2_halves(x.w, dot2_halves(x.z, dot2_halves(x.y, dot2_halves(x.x, acc))));
 }
+// sum_range() as a sum of 16-bit halves (< 2^20; no 64-bit adds, no fold needed before a DPP reduction)
+__device__ __forceinline__ uint32_t sum_range_h(u32x4 x, int ro, int lo, int hi) {
+    uint32_t acc = dot2_halves(keep_bytes(x.x, ro, lo, hi), 0u);
+    acc = dot2_halves(keep_bytes(x.y, ro + 4, lo, hi), acc);
+    acc = dot2_halves(keep_bytes(x.z, ro + 8, lo, hi), acc);
+    return dot2_halves(keep_bytes(x.w, ro + 12, lo, hi), acc);
+}
 // sum of the bytes of block x (row bytes [ro, ro+16)) that lie in [lo, hi)
 __device__ __forceinline__ uint64_t sum_range(u32x4 x, int ro, int lo, int hi) {
     return (uint64_t)keep_bytes(x.x, ro, lo, hi) + (uint64_t)keep_bytes(x.y, ro + 4, lo, hi) +
@@ -233,7 +240,7 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
 // Header work of one frame (lane = frame) from its LDS row and its two folded row sums.  DEFER: the
 // verdict and record are returned in *verd_out / *rec_out instead of being stored (the round kernel
 // stores them in its write phase).
-template <bool DEFER = false, bool IPH = false>
+template <bool DEFER = false, bool IPH = false, bool FASTIP = false>
 __device__ __forceinline__ bool header_phase5(const EchoArgs& a, uint8_t* row, uint32_t ip_raw, uint32_t ic_raw,
                                               uint64_t addr, uint32_t len, bool live, bool ok, bool parse,
                                               uint32_t fi, Counters& cnt, u32x4* rec_out = nullptr,
@@ -278,8 +285,13 @@ __device__ __forceinline__ bool header_phase5(const EchoArgs& a, uint8_t* row, u
                 // frame-even-aligned words are byte-swapped network words (RFC 1071 §2(B))
         const int e = (int)min(len, 34u);
         uint32_t acc = 0;
+        if (FASTIP && __ballot(e < 34) == 0ull) {  // every frame has the whole 20-B header: fixed masks
+            acc = dot2_halves(h[3] >> 16, dot2_halves(h[4], dot2_halves(h[5], 0u)));
+            acc = dot2_halves(h[8] & 0xFFFFu, dot2_halves(h[7], dot2_halves(h[6], acc)));
+        } else {
 #pragma unroll
-        for (int kk = 3; kk <= 8; ++kk) acc += halves(keep_bytes(h[kk], 4 * kk, 14, e));
+            for (int kk = 3; kk <= 8; ++kk) acc += halves(keep_bytes(h[kk], 4 * kk, 14, e));
+        }
         ip_sum = bswap16(fold32(acc));
     }
     uint32_t flags = 0;
@@ -375,6 +387,7 @@ constexpr int kShip6TPW = 2;                // tiles per wave per round: 2048 fr
 constexpr int kShip6Sync = 2;               // heavy waves wait for the round, light ones go ahead
 constexpr int kShip6Stream = 2;             // per-step streams for uniform long tiles, sorted step-packed otherwise
 constexpr bool kShip6Mid = true;            // ping-size tiles (every frame within 128 B): 8 loads at once
+constexpr bool kShip6D2 = true;             // v_dot2_u32_u16 sums of halves (short, ping and per-step paths)
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -942,15 +955,19 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
                         *(u32x4*)(rows + f * kRowW + ro) = v;
                         const int f_off = (int)(f_packed & 0xFFu), f_iphi = (int)((f_packed >> 8) & 0xFFu);
-                        uint32_t rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
-                        uint32_t ric = fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
-                        rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);
+                        // D2: the IPv4 header sum comes from the window in the header phase (STREAM >= 1)
+                        constexpr bool kRip = !(D2 && STREAM >= 1);
+                        uint32_t rip = 0u;
+                        if (kRip) rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
+                        uint32_t ric = D2 ? sum_range_h(v, (int)ro, f_off + 34, (int)fm.rowhi)
+                                          : fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
+                        if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);
-                        rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0x4E, 0xF, 0xF, false);
+                        if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0x4E, 0xF, 0xF, false);
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);
                         if (kk == 0u) {
                             sums_ic[f] = ric;
-                            sums_ip[f] = rip;
+                            if (kRip) sums_ip[f] = rip;
                         }
                     }
                 } else if (MID && !WIRE && mid_tile) {
@@ -971,7 +988,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         const FrameMeta6& fm = meta[f];
                         const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
                         if (kk < 4u) *(u32x4*)(rows + f * kRowW + ro) = v;
-                        uint32_t ric = fold64(sum_range(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi));
+                        uint32_t ric = D2 ? sum_range_h(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi)
+                                          : fold64(sum_range(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi));
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);   // xor 1
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);   // xor 2
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x141, 0xF, 0xF, false);  // half-row mirror
@@ -986,8 +1004,9 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                 } else if (STREAM == 1 ||
                            (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                             uniform(max_nit_lane(nit)) < (uint32_t)U))) {
-                    if (fast) stream_tile_sorted<U, true, WIRE, D2>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted<U, false, WIRE, D2>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
+                    if (fast) stream_tile_sorted<U, true, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted<U, false, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else {
                     for (uint32_t s = 0; s < 16; ++s) {
                         const uint32_t f = 4u * s + q;
@@ -1028,7 +1047,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                 wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, fi < a.n, wend, cnt, &rec[i],
                                        &verd[i]);
             else
-                wb = header_phase5<true, STREAM >= 1>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, fi < a.n, ok,
+                wb = header_phase5<true, STREAM >= 1, D2>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, fi < a.n, ok,
                                                        parse, fi, cnt, &rec[i], &verd[i]);
             wbm[i] = __ballot(wb);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
