@@ -313,7 +313,7 @@ extern "C" {
 uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip
 
 int xsk_gpu__set_wire_impl(int impl) {
-    if (impl < 0 || impl > 1) return -EINVAL;
+    if (impl < 0 || impl > 2) return -EINVAL;
     g_wire_impl = impl;
     return 0;
 }
@@ -344,6 +344,9 @@ int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gp
     if (g_wire_impl == 0)
         echo_kernel6<kShip6U, 1, 2, 2, false, false, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(
             args, tiles_per_wg);
+    else if (g_wire_impl == 2)  // + dot2 sums in the per-step streams
+        echo_kernel6<kShip6U, 1, 2, 2, false, false, true, false, false, false, true>
+            <<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, tiles_per_wg);
     else
         echo_wire_kernel<kWireU, kWaves6, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, opts,
                                                                                                        tiles_per_wg);
