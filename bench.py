@@ -25,7 +25,7 @@ import torch  # noqa: E402
 
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true>"  # the transform kernel xsk_gpu_echo_dev launches
+KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true>"  # the transform kernel xsk_gpu_echo_dev launches
 WIRE_KERNEL = "echo_kernel6<4, 1, 2, 2, false, false, true, false, false>"  # xsk_gpu_echo_dev_opts, nonzero --opts
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
@@ -141,6 +141,9 @@ def traffic_from_profiles(cfg, kernel):
     (tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled on gfx950),
     or None when there is none for the kernel that ran."""
     p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    env = os.environ.get("XSK_TRAFFIC_JSON")  # a fresh summary of this build (tools/gpu_full.sh)
+    if env and os.path.basename(env) == os.path.basename(p):
+        p = env
     try:
         d = json.load(open(p))
     except (OSError, ValueError):

@@ -140,7 +140,8 @@ static int echo_dev_impl(void* d_umem, uint64_t umem_size, const struct xsk_gpu_
 
     const int slot = timer_slot(device);
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
-    echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2>
+    echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2,
+                 kShip6Skm>
         <<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     HIP_TRY(hipGetLastError());
     if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], s));

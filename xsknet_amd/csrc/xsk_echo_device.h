@@ -388,6 +388,7 @@ constexpr int kShip6Sync = 2;               // heavy waves wait for the round, l
 constexpr int kShip6Stream = 2;             // per-step streams for uniform long tiles, sorted step-packed otherwise
 constexpr bool kShip6Mid = true;            // ping-size tiles (every frame within 128 B): 8 loads at once
 constexpr bool kShip6D2 = true;             // v_dot2_u32_u16 sums of halves (short, ping and per-step paths)
+constexpr bool kShip6Skm = true;            // ranked streams mask only slots where a frame ends
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -407,7 +408,7 @@ __device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
 // (ragged batches waste fewer lanes), and each batch of U row-loads is packed across consecutive steps
 // by a wave-uniform cursor (short frames share one round trip instead of paying one per step).  The
 // IPv4 header sum is taken in the header phase from the LDS window (header_phase5<.., IPH = true>).
-template <int U, bool FAST, bool WIRE = false, bool D2 = false>
+template <int U, bool FAST, bool WIRE = false, bool D2 = false, bool SKM = false>
 __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
                                                    const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
                                                    uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
@@ -493,10 +494,14 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
             } else {
                 const int nb = (int)(urowhi[u] - min(ro, urowhi[u]));
                 u32x4 y = x;
-                y.x &= dw_mask(nb);
-                y.y &= dw_mask(nb - 4);
-                y.z &= dw_mask(nb - 8);
-                y.w &= dw_mask(nb - 12);
+                // SKM: blocks past row 0 are whole (nb >= 16) or zeros (not loaded) unless one of the slot's
+                // frames ends inside it -- mask only then (wave-uniform test, as in stream_frame)
+                if (!SKM || __ballot(nb > 0 && nb < 16) != 0ull) {
+                    y.x &= dw_mask(nb);
+                    y.y &= dw_mask(nb - 4);
+                    y.z &= dw_mask(nb - 8);
+                    y.w &= dw_mask(nb - 12);
+                }
                 if (D2) h = sum_halves(y, h);
                 else ic += sum_dw(y);
             }
@@ -810,7 +815,7 @@ constexpr uint32_t kHeavyLen = 1024;
 // NTS (tuning): write-phase stores nontemporal.  NOWR (tuning, wrong results): skip the write phase,
 // to time the read phase alone.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false>
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
@@ -1005,8 +1010,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                            (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                             uniform(max_nit_lane(nit)) < (uint32_t)U))) {
                     // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
-                    if (fast) stream_tile_sorted<U, true, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted<U, false, WIRE>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    if (fast) stream_tile_sorted<U, true, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    else stream_tile_sorted<U, false, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                 } else {
                     for (uint32_t s = 0; s < 16; ++s) {
                         const uint32_t f = 4u * s + q;

@@ -385,6 +385,7 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 89: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 90: echo_kernel6<4, 2, 3, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 91: echo_kernel6<4, 2, 4, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 92: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
