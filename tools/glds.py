@@ -17,7 +17,9 @@ L.glds_run.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, 
                        C.c_void_p]
 
 NAMES = {0: "reg U4", 1: "reg U8", 2: "glds U4 nt", 3: "glds U8 nt", 4: "glds U4 default", 5: "glds U8 default",
-         6: "glds U16 nt"}
+         6: "glds U16 nt", 7: "per-WG contiguous reg U4", 8: "per-WG contiguous reg U8", 9: "per-WG contiguous reg U2"}
+KINDS = [int(k) for k in os.environ.get("GLDS_KINDS", ",".join(map(str, NAMES))).split(",")]
+GRIDS = {k: ((256,) if k >= 7 else (1024, 2048)) for k in NAMES}
 
 
 def main():
@@ -27,12 +29,16 @@ def main():
     out = torch.zeros(1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream().cuda_stream
     rows = (ln + 255) // 256
-    cases = [("contig_1.5GB", 0, n * ln // 1024), ("c3_rows_s4096", 1, n // 4 * rows)]
+    cases = [("contig_1.5GB", 0, n * ln // 1024), ("c3_rows_s4096", 1, n // 4 * rows),
+             ("c3_framemajor_s4096", 2, n * 2), ("c3_rows128_s4096", 3, n // 8 * ((ln + 127) // 128))]
+    only = os.environ.get("GLDS_CASES")
+    if only:
+        cases = [c for c in cases if c[0] in only.split(",")]
     res = {}
     for rep in range(8):
         for cname, layout, npieces in cases:
-            for kind in NAMES:
-                for grid in (1024, 2048):
+            for kind in KINDS:
+                for grid in GRIDS[kind]:
                     for s in slabs:
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
