@@ -415,9 +415,23 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (window) bytes
     const uint32_t q = lane >> 4, k = lane & 15u;
     uint32_t rank = 0;
-    for (uint32_t j = 0; j < 64u; ++j) {
-        const uint32_t nj = rdlane(nit_own, j);
-        rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
+    if (SKM && __ballot(nit_own > 7u) == 0ull) {
+        // counting rank (every frame <= 7 row-loads, i.e. up to ~1.8 KB): per value v one ballot; rank =
+        // lanes with fewer row-loads + lanes below with as many (same order as the compare loop below)
+        uint32_t below = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < 8u; ++v) {
+            const uint64_t bv = __ballot(nit_own == v);
+            const uint32_t cv = (uint32_t)__popcll(bv);
+            const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(bv >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bv, 0u));
+            if (nit_own == v) rank = below + mb;
+            below += cv;
+        }
+    } else {
+        for (uint32_t j = 0; j < 64u; ++j) {
+            const uint32_t nj = rdlane(nit_own, j);
+            rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
+        }
     }
     sort[rank] = lane;                                    // sort[0..63]: frame of rank r
     if ((rank & 3u) == 3u) sort[64u + (rank >> 2)] = nit_own;  // sort[64 + s]: row-loads of step s
