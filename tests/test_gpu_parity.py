@@ -124,6 +124,16 @@ def test_valid_parity_layouts(stride, lo, hi):
     assert (v == 0).all()
 
 
+@pytest.mark.parametrize("off,ln", [(2, 60), (6, 98), (13, 98), (9, 64), (0, 112)])
+def test_uniform_tiles_at_offsets(off, ln):
+    """Tiles of identical frames at one 16-B offset (c2 / ping shapes): the per-tile byte-mask path."""
+    n, stride = 4096, 2048
+    umem = np.zeros(n * stride + 64, np.uint8)
+    descs = oracle.synth_batch(umem, n, off, stride, seed=0x5EED0C0C + off, mode=0, len_lo=ln, len_hi=ln)
+    v = check_against_oracle(umem, descs)
+    assert (v == 0).all()
+
+
 def test_unaligned_non_uniform_addresses():
     """Frames at random byte offsets (odd ones too) inside 4 KiB chunks, in shuffled order."""
     rng = np.random.default_rng(1)

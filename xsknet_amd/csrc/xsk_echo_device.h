@@ -156,6 +156,11 @@ __device__ __forceinline__ uint32_t dot2_halves(uint32_t v, uint32_t acc) {
 __device__ __forceinline__ uint32_t sum_halves(u32x4 x, uint32_t acc) {
     return dot2_halves(x.w, dot2_halves(x.z, dot2_halves(x.y, dot2_halves(x.x, acc))));
 }
+// Byte-keep masks of block [ro, ro+16) for the range [lo, hi) (keep_bytes of all-ones per dword).
+__device__ __forceinline__ u32x4 range_mask(int ro, int lo, int hi) {
+    return u32x4{keep_bytes(~0u, ro, lo, hi), keep_bytes(~0u, ro + 4, lo, hi), keep_bytes(~0u, ro + 8, lo, hi),
+                 keep_bytes(~0u, ro + 12, lo, hi)};
+}
 // sum_range() as a sum of 16-bit halves (< 2^20; no 64-bit adds, no fold needed before a DPP reduction)
 __device__ __forceinline__ uint32_t sum_range_h(u32x4 x, int ro, int lo, int hi) {
     uint32_t acc = dot2_halves(keep_bytes(x.x, ro, lo, hi), 0u);
@@ -913,6 +918,10 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
             const uint32_t nit = (lim + 255u) >> 8;
             const bool short_tile = __ballot(lim > kRowW) == 0ull;
             const bool mid_tile = MID && !WIRE && !short_tile && __ballot(lim > 128u) == 0ull;
+            // SKM: every frame of the tile at the same 16-B offset with the same end (c2, pings): the ICMP
+            // byte masks of a lane's block are the same for all its frames -> computed once per tile
+            const uint32_t ukey = (off << 24) ^ rowhi;
+            const bool uni_tile = SKM && !WIRE && (short_tile || mid_tile) && __ballot(ukey != uniform(ukey)) == 0ull;
             uint64_t wlo = 0, span = ~0ull;
             if (!short_tile) {
                 wlo = wave_min_u64(nit ? a16 : ~0ull);
@@ -942,6 +951,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                     // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
                     // nothing lies past byte 128, so the streamed part of every sum is zero
                     const uint32_t kk = lane & 7u, ro = 16u * kk;
+                    const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
                     u32x4 x[8];
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
@@ -959,6 +969,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                 } else if (short_tile) {
                     // every frame within its 64-B window: 4 lanes per frame, 16 frames per wave-load
                     const uint32_t kk = lane & 3u, ro = 16u * kk;
+                    const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
                     u32x4 x[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -978,7 +989,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         constexpr bool kRip = !(D2 && STREAM >= 1);
                         uint32_t rip = 0u;
                         if (kRip) rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
-                        uint32_t ric = D2 ? sum_range_h(v, (int)ro, f_off + 34, (int)fm.rowhi)
+                        uint32_t ric = (SKM && uni_tile) ? sum_halves(v & umk, 0u)
+                                     : D2 ? sum_range_h(v, (int)ro, f_off + 34, (int)fm.rowhi)
                                           : fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
                         if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);
@@ -994,6 +1006,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                     // per wave-load, all 8 loads in flight at once; the ICMP sum by exact byte range, reduced
                     // over the 8 lanes (the IPv4 header sum comes from the window in the header phase)
                     const uint32_t kk = lane & 7u, ro = 16u * kk;
+                    const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
                     u32x4 x[8];
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
@@ -1007,7 +1020,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                         const FrameMeta6& fm = meta[f];
                         const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
                         if (kk < 4u) *(u32x4*)(rows + f * kRowW + ro) = v;
-                        uint32_t ric = D2 ? sum_range_h(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi)
+                        uint32_t ric = (SKM && uni_tile) ? sum_halves(v & umk, 0u)
+                                     : D2 ? sum_range_h(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi)
                                           : fold64(sum_range(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi));
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);   // xor 1
                         ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);   // xor 2
