@@ -821,6 +821,8 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
 // all write); 2: a wave whose tiles averaged >= kHeavyLen bytes per frame waits until every wave of
 // the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
 // phase separation pays where reads dominate, and costs latency hiding where frames are short.
+// 3 / 4 (tuning only): a chip-wide barrier before (3) or around (4) every write phase, on a counter the
+// host zeroes at partials + 64 Ki (measured 4-80 % slower).
 constexpr uint32_t kHeavyLen = 1024;
 // STREAM: 0 = per-step row streams (stream_frame), 1 = sorted step-packed streams (stream_tile_sorted),
 // 2 = per tile: per-step streams when every parsed frame needs the same number (>= U) of row-loads
@@ -833,6 +835,12 @@ constexpr uint32_t kHeavyLen = 1024;
 // WIRE: the wire-format mode (a.opts != 0): 128-B windows (so TPW 1), wire_header_phase.
 // NTS (tuning): write-phase stores nontemporal.  NOWR (tuning, wrong results): skip the write phase,
 // to time the read phase alone.
+// MID: tiles whose frames all lie within 128 B of their 16-B aligned starts (pings) are read by 8-lane
+// groups, 8 frames per wave-load, all 8 loads in flight.
+// D2: sums of 16-bit halves with v_dot2_u32_u16 in the per-step streams, the short and ping-size paths;
+// the header phase's IPv4 sum with fixed masks when every frame has its whole header.
+// SKM: ranked streams mask only slots where a frame ends and rank small-row tiles by counting; uniform
+// short / ping-size tiles compute their ICMP byte masks once per tile.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
