@@ -1,5 +1,7 @@
 # Build of the MI355X (gfx950) echo-transform library and its C tools.
-#   make            -> xsknet_amd/libxsknet_amd.so, oracle/liboracle.so, tools/echo_replay
+#   make            -> xsknet_amd/libxsknet_amd.so (the product), xsknet_amd/libxsknet_amd_tune.so (kernel
+#                      variants for tools/kbench.py and their parity tests only), oracle/liboracle.so,
+#                      tools/echo_replay
 ROCM     ?= /opt/rocm
 HIPCC    ?= $(ROCM)/bin/hipcc
 CC       := gcc
@@ -8,23 +10,30 @@ HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall
 CFLAGS   ?= -O2 -std=c11 -Wall -Wextra -fPIC
 CSRC     := xsknet_amd/csrc
 LIB      := xsknet_amd/libxsknet_amd.so
+TUNELIB  := xsknet_amd/libxsknet_amd_tune.so
 
-all: $(LIB) oracle tools/echo_replay
+all: $(LIB) $(TUNELIB) oracle tools/echo_replay
 
-DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_variants.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
-HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_tune.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_wire.o
+DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
+HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_lowlat.o
+HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o
+TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(CSRC)/xsk_gpu_host.o: $(CSRC)/xsk_gpu_host.c include/xsk_gpu.h
-	$(CC) $(CFLAGS) -I$(ROCM)/include -c -o $@ $<
+$(CSRC)/tune/%.o: $(CSRC)/tune/%.hip $(DEVHDR) $(CSRC)/tune/xsk_echo_variants.h
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-$(CSRC)/xsk_gpu_rx.o: $(CSRC)/xsk_gpu_rx.c $(CSRC)/xsk_ring.h include/xsk_gpu.h
-	$(CC) $(CFLAGS) -c -o $@ $<
+$(CSRC)/%.o: $(CSRC)/%.c include/xsk_gpu.h $(CSRC)/xsk_gpu_internal.h $(CSRC)/xsk_ring.h
+	$(CC) $(CFLAGS) -pthread -I$(ROCM)/include -c -o $@ $<
 
-$(LIB): $(HIPOBJ) $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,libxsknet_amd.so
+$(LIB): $(HIPOBJ) $(HOSTOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -pthread -Wl,-soname,libxsknet_amd.so
+
+$(TUNELIB): $(TUNEOBJ) $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(TUNEOBJ) -L xsknet_amd -lxsknet_amd \
+		-Wl,-rpath,'$$ORIGIN' -Wl,-soname,libxsknet_amd_tune.so
 
 tools/echo_replay: tools/echo_replay.c $(LIB) include/xsk_gpu.h
 	$(CC) $(CFLAGS) -o $@ $< -L xsknet_amd -lxsknet_amd -Wl,-rpath,'$$ORIGIN/../xsknet_amd'
@@ -33,7 +42,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(CSRC)/*.o $(LIB) tools/echo_replay
+	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

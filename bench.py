@@ -7,13 +7,18 @@ gets a fresh, never-transformed batch (a pool of pre-generated batches), so no s
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4|c5|p98] [--no-cpu] [--host-inclusive]
 
-Multi-GPU: one process per GPU (torch.distributed.run); frame i of a step's global batch goes to
-GPU i mod N (round-robin sharding, no data-path collective); per-GPU work is fixed -> weak scaling.
-Rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU.  Run as `python bench.py --gpus N` (no launcher) the script starts
+`torch.distributed.run --nproc-per-node N` itself as a child process before anything touches a GPU, and
+exits with its status; under an external torch.distributed.run it is one of the ranks and checks that
+WORLD_SIZE == N.  Frame i of a step's global batch goes to GPU i mod N (round-robin sharding, no
+data-path collective): c2/c3/c4/p98 keep the per-GPU work fixed (weak scaling), c5 splits a fixed 64 M
+frames per step over the N GPUs (strong scaling).  Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -51,12 +56,25 @@ def log(*a):
 SHARE_GPU = os.environ.get("XSK_BENCH_SHARE_GPU") == "1"
 
 
+def launch_ranks(gpus):
+    """Start `torch.distributed.run` with one rank per GPU as a child process (this process has not
+    touched a GPU and never will) and return its exit status; rank 0's JSON line reaches our stdout."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[launcher] {gpus} ranks: {' '.join(cmd[1:5])} ...")
+    return subprocess.run(cmd).returncode
+
+
 def dist_setup(gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if SHARE_GPU else int(os.environ.get("LOCAL_RANK", "0"))
     if world != gpus:
-        log(f"warning: --gpus {gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: run `python bench.py --gpus {gpus}` "
+                         f"(it starts its own ranks) or launch {gpus} ranks")
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
@@ -83,46 +101,96 @@ def barrier(world):
         dist.barrier()
 
 
-def cpu_baseline(cfg, budget_s=12.0):
-    """Oracle C port timed on this host's cores on a bounded sample of the same workload."""
+def cpu_share():
+    """CPUs this process may use: the affinity mask, bounded by the cgroup CPU quota (on the GPU box the
+    machine's nproc is many times the box's share), and never above 16 (the pool's worker-pool rule)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    share = min(n, quota) if quota else n
+    return max(1, min(16, share)), n, quota
+
+
+def _read(path):
+    try:
+        return open(path).read().strip()
+    except OSError:
+        return None
+
+
+def cpu_baseline(cfg, budget_s=8.0):
+    """The oracle's C restatement timed on this host's cores on a bounded sample of the same workload:
+    full contract (gates, rewrite, RFC 1071 full-payload sums, records, counters) and the reference-
+    equivalent header-only transform (process_packet without logging / sendto), each at 1 thread and
+    at the box's CPU share, plus BASELINE config 1 (4096 x 64 B, one UMEM) replayed in-process."""
     import oracle
     n_total, lo, hi, stride, seed, _ = CONFIGS[cfg]
-    threads = max(1, min(16, os.cpu_count() or 1))
+    share, affinity, quota = cpu_share()
     n = min(n_total, 1 << 17)  # 131072 frames
     umem = np.zeros(n * stride, np.uint8)
-    descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi)
+    descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi, threads=share)
     nbytes = int(descs["len"].sum())
 
-    def run(fn, budget):
+    def run(fn, budget, um=umem, ds=descs):
         done, t_tot = 0, 0.0
         while t_tot < budget:
             t0 = time.perf_counter()
-            v = fn()
+            v = fn(um, ds)
             t_tot += time.perf_counter() - t0
-            done += n
-            oracle.rearm(umem, descs, v)  # untimed: restore requests for the next pass
-        return done, t_tot
+            done += len(ds)
+            oracle.rearm(um, ds, v)  # untimed: restore requests for the next pass
+        return done / t_tot / 1e6
 
-    def full_mt():
-        return oracle.echo_batch(umem, descs, threads=threads)[0]
+    def full(threads):
+        return lambda um, ds: oracle.echo_batch(um, ds, threads=threads)[0]
 
-    def hdr_1t():
-        verd = np.zeros(n, np.uint8)
-        st = np.zeros(1, oracle.STATS_DTYPE)
-        oracle.lib().oracle_echo_batch_hdr(umem.ctypes.data, descs.ctypes.data, n, verd.ctypes.data, st.ctypes.data)
-        return verd
+    def hdr(threads):
+        def f(um, ds):
+            verd = np.zeros(len(ds), np.uint8)
+            st = np.zeros(1, oracle.STATS_DTYPE)
+            oracle.lib().oracle_echo_batch_hdr_mt(um.ctypes.data, ds.ctypes.data, len(ds), verd.ctypes.data,
+                                                  st.ctypes.data, threads)
+            return verd
+        return f
 
-    d1, t1 = run(full_mt, budget_s)
-    d2, t2 = run(hdr_1t, budget_s / 4)
+    full_n = run(full(share), budget_s)
+    full_1 = run(full(1), budget_s / 2)
+    hdr_n = run(hdr(share), budget_s / 4)
+    hdr_1 = run(hdr(1), budget_s / 4)
+    # BASELINE config 1: 4096 x 64 B in one 16 MiB UMEM of 4 KiB chunks (256-B headroom), in-process
+    c1_umem = np.zeros(4096 * 4096, np.uint8)
+    c1_descs = oracle.synth_batch(c1_umem, 4096, 256, 4096, 0x5EED0001, mode=0, len_lo=64, len_hi=64)
+    c1_hdr = run(hdr(1), budget_s / 4, c1_umem, c1_descs)
+    c1_full = run(full(1), budget_s / 4, c1_umem, c1_descs)
+    gib = nbytes / n / 2**30
     return {
-        "value": round(d1 / t1 / 1e6, 3), "unit": "Mframes/s", "cores": threads, "kind": "port",
-        "gib_per_s": round(d1 / n * nbytes / t1 / 2**30, 3),
-        "sample": f"{n} frames of {cfg} ({lo}-{hi} B, stride {stride}), full contract (gates, rewrite, "
-                  f"RFC1071 full-payload sums, records, counters), {threads} pthreads, {t1:.1f} s",
-        "reference_equivalent_1core": {"value": round(d2 / t2 / 1e6, 3), "unit": "Mframes/s", "cores": 1,
-                                       "sample": "header-only transform exactly as process_packet "
-                                                 "(no logging, no sendto, no payload sums)"},
-        "cpu_model": _cpu_model(),
+        "value": round(full_n, 3), "unit": "Mframes/s", "cores": share, "kind": "port",
+        "gib_per_s": round(full_n * 1e6 * gib, 3),
+        "sample": f"{n} frames of {cfg} ({lo}-{hi} B, stride {stride}), full contract (gates, rewrite, RFC 1071 "
+                  f"full-payload sums, records, counters) of oracle/echo_oracle.c, {share} pthreads over contiguous "
+                  f"frame ranges",
+        "full_contract_1core": round(full_1, 3),
+        "reference_equivalent": {"cores": share, "value": round(hdr_n, 3), "value_1core": round(hdr_1, 3),
+                                 "unit": "Mframes/s",
+                                 "sample": "header-only transform exactly as process_packet (no logging, no sendto, "
+                                           "no payload sums)"},
+        "c1_in_process": {"workload": "BASELINE configs[0]: 4096 x 64 B ICMP echo requests, one per 4 KiB chunk of a "
+                                      "16 MiB UMEM (256-B headroom), replayed in-process (no veth / XDP / sendto)",
+                          "reference_equivalent_1core": round(c1_hdr, 3), "full_contract_1core": round(c1_full, 3),
+                          "unit": "Mframes/s"},
+        "host": {"cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity,
+                 "cgroup_cpu_quota": quota, "smt_active": _read("/sys/devices/system/cpu/smt/active"),
+                 "threads_used": share,
+                 "note": "threads = this box's CPU share (affinity / cgroup quota, at most 16: the GPU pool's "
+                         "worker rule), not the machine's nproc"},
     }
 
 
@@ -160,9 +228,16 @@ def host_inclusive(cfg, dev_index):
     umem = np.zeros(n * stride, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi)
     out = {}
-    for name, mode in (("staged", X.MODE_STAGED), ("zerocopy", X.MODE_ZEROCOPY)):
+    ndev = torch.cuda.device_count()
+    runs = [("staged", X.MODE_STAGED, None), ("zerocopy", X.MODE_ZEROCOPY, None)]
+    for g in (1, 2):  # xsk_gpu_multi over G contexts: distinct GPUs when there are, else G on this one
+        devs = list(range(dev_index, dev_index + g)) if dev_index + g <= ndev else [dev_index] * g
+        runs.append((f"staged_multi_g{g}", X.MODE_STAGED, devs))
+    for name, mode, devs in runs:
         work = umem.copy()
-        with X.EchoContext(work, dev_index, max_batch=n, mode=mode) as ctx:
+        mk = (lambda: X.EchoContext(work, dev_index, max_batch=n, mode=mode)) if devs is None else \
+            (lambda: X.MultiContext(work, devs, max_batch=n, mode=mode))
+        with mk() as ctx:
             ctx.process(descs, want_recs=False)  # warm
             v = None
             reps, t = 0, 0.0
@@ -174,6 +249,8 @@ def host_inclusive(cfg, dev_index):
                 reps += 1
         out[name] = {"mframes_per_s": round(reps * n / t / 1e6, 3),
                      "gib_per_s": round(reps * int(descs["len"].sum()) / t / 2**30, 3), "frames_per_call": n}
+        if devs is not None:
+            out[name]["devices"] = devs
     return out
 
 
@@ -189,14 +266,14 @@ def main():
     ap.add_argument("--opts", type=int, default=0,
                     help="wire-format options (XSK_GPU_OPT_*, xsk_gpu_echo_dev_opts); 0 = the reference's gates")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))  # nothing has touched a GPU in this process
 
     import xsknet_amd as X
     from xsknet_amd import shard
     X.lib()  # fail loudly if the HIP library is missing
-    if os.environ.get("XSK_WIRE_IMPL"):  # tuning only: 1 = the window-first wire kernel, for comparison
-        import ctypes
-        X.lib().xsk_gpu__set_wire_impl.argtypes = [ctypes.c_int]
-        assert X.lib().xsk_gpu__set_wire_impl(int(os.environ["XSK_WIRE_IMPL"])) == 0
 
     rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", local)
@@ -234,7 +311,8 @@ def main():
     log(f"[rank {rank}] generated {pool} batches in {time.perf_counter() - t0:.1f} s")
     frame_bytes = int(descss[0].view(torch.int32).view(-1, 4)[:, 2].to(torch.int64).sum().item())
 
-    verd = torch.empty(n, dtype=torch.uint8, device=dev)
+    # one verdict buffer per pooled batch: a re-arm restores batch b from ITS verdicts of its previous use
+    verds = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(pool if rearm_in_loop else 1)]
     recs = torch.empty(n * 16, dtype=torch.uint8, device=dev)
     stats = torch.zeros(40, dtype=torch.uint8, device=dev)
     ws = torch.zeros(max(16, X.workspace_size(local, n)), dtype=torch.uint8, device=dev)
@@ -242,6 +320,7 @@ def main():
 
     def step(s):
         b = s % pool
+        verd = verds[b % len(verds)]
         if rearm_in_loop and s >= pool:
             X.rearm_dev(umems[b], descss[b], verd, n, stream)  # conservative: counted inside the timing
         X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream, opts=args.opts)
@@ -281,8 +360,7 @@ def main():
     # ---- correctness of what was timed: every frame of every step accepted and counted ----
     st = stats.cpu().numpy().view(X.STATS_DTYPE)[0]
     ok = int(st["rx_packets"]) == (W + K) * n and int(st["tx_packets"]) == (W + K) * n
-    vr = verd.cpu().numpy()
-    ok = ok and bool((vr == 0).all())
+    ok = ok and all(bool((v == 0).all().item()) for v in verds)
     recs_np = recs.cpu().numpy().view(X.REC_DTYPE)
     ok = ok and bool((recs_np["flags"] == 3).all())
 

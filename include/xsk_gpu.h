@@ -182,8 +182,18 @@ enum xsk_gpu_mode {
     /* The frames' UMEM span is copied host->device, transformed in HBM, and the 64-byte header
      * window of every frame is copied back (strided 2-D copy when the batch has a uniform
      * stride).  Best for large batches. */
-    XSK_GPU_MODE_STAGED = 1
+    XSK_GPU_MODE_STAGED = 1,
+    /* ZEROCOPY data path plus a resident polling kernel for the RX loop's small batches: a call with
+     * n <= XSK_GPU_LOWLAT_MAX writes the descriptors into mapped host memory, bumps a doorbell the
+     * kernel polls, and spins until the kernel publishes completion -- no launch, no stream sync.  The
+     * kernel runs the launched kernel's code (bit-identical results), holds one CU while it serves, and
+     * exits on xsk_gpu_fini() or after 50 ms without a batch (the next call relaunches it).  Larger
+     * batches stop it and take the ZEROCOPY launch path. */
+    XSK_GPU_MODE_LOWLAT = 2
 };
+
+/* Largest batch the LOWLAT doorbell takes (larger ones are launched). */
+#define XSK_GPU_LOWLAT_MAX 1024u
 
 /* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
  * xsk_utils.c:132-135).  The UMEM is page-locked (hipHostRegister) until xsk_gpu_fini().
@@ -201,6 +211,33 @@ int xsk_gpu_set_options(xsk_gpu_ctx* ctx, uint32_t opts);
 
 /* Release device buffers and unregister the UMEM. NULL is a no-op. */
 void xsk_gpu_fini(xsk_gpu_ctx* ctx);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Several GPUs behind one RX loop: one UMEM, G contexts.                       */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct xsk_gpu_multi xsk_gpu_multi;
+
+#define XSK_GPU_MULTI_MAX 16
+
+/* Bind G = ndev contexts (devices[g], repeats allowed: G contexts on one GPU) to ONE caller UMEM
+ * (registered once with the HIP runtime, portable + mapped, for every device).  `mode` and
+ * `max_batch` as for xsk_gpu_init(); max_batch bounds the whole batch of later calls. */
+int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, void* umem, uint64_t umem_size,
+                       uint32_t max_batch, int mode);
+
+/* xsk_gpu_process() of one batch over the G contexts: descriptor i goes to context i mod G (frames
+ * are independent, xsk_receive.c:113-190), each context runs on its own host thread and stream, and
+ * verdicts / records land at the descriptors' own positions.  The four counters are the sum over the
+ * contexts (xsk_utils.h:17-23), added to *stats like xsk_gpu_process() does. */
+int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
+                          struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+
+/* Wire-format options for every context (xsk_gpu_set_options). */
+int xsk_gpu_multi_set_options(xsk_gpu_multi* m, uint32_t opts);
+
+/* Stop the worker threads, release every context, unregister the UMEM.  NULL is a no-op. */
+void xsk_gpu_multi_fini(xsk_gpu_multi* m);
 
 /* ------------------------------------------------------------------------------------------ */
 /* XDP ingress filter on the device (the frames the echo transform sees).                      */
@@ -268,7 +305,8 @@ struct xsk_gpu_rx_result {
 /* One pass of handle_receive_packets() (src/lib/xsk_receive.c:192-237) with the transform on the
  * GPU and the XSK TX path the reference leaves commented out (:174-186) enabled instead of the
  * per-frame sendto() (:166):
- *   1. peek up to min(max_batch, XSK_GPU_RX_MAX_STEP) RX descriptors (:196); none -> return 0;
+ *   1. peek up to min(max_batch, XSK_GPU_RX_MAX_STEP, the context's max_batch) RX descriptors (:196);
+ *      none -> return 0;
  *   2. refill the fill ring with min(free fill slots, free frames) frames from `pool` (:201-217;
  *      the reference reserves the free-slot count even when it has fewer free frames);
  *   3. xsk_gpu_process() the batch (replaces the per-frame process_packet() loop :220-230);

@@ -38,6 +38,15 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
+def cpu_threads() -> int:
+    """Worker threads for the oracle on this host: the CPUs this process may run on (the GPU box's share
+    of a large machine is smaller than os.cpu_count())."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1)
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
@@ -57,6 +66,8 @@ def lib() -> C.CDLL:
                                    C.c_uint32),
             "oracle_synth_batch": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                     C.c_uint64, C.c_int, C.c_uint32, C.c_uint32], C.c_int),
+            "oracle_synth_batch_mt": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                       C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, C.c_int], C.c_int),
             "oracle_rearm": ([_P, _P, _P, C.c_uint32], None),
             "oracle_mix64": ([C.c_uint64], C.c_uint64),
             "oracle_xdp_classify": ([_P, C.c_uint32, C.c_int], C.c_int),
@@ -116,10 +127,14 @@ def echo_batch_opts(umem: np.ndarray, descs: np.ndarray, opts: int):
 
 
 def synth_batch(umem: np.ndarray, n: int, base_off: int, stride: int, seed: int, first: int = 0, step: int = 1,
-                mode: int = 0, len_lo: int = 1500, len_hi: int = 1500) -> np.ndarray:
+                mode: int = 0, len_lo: int = 1500, len_hi: int = 1500, threads: int = 1) -> np.ndarray:
     descs = np.zeros(n, DESC_DTYPE)
-    rc = lib().oracle_synth_batch(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, base_off, stride, seed, first,
-                                  step, mode, len_lo, len_hi)
+    if threads > 1:
+        rc = lib().oracle_synth_batch_mt(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, base_off, stride, seed,
+                                         first, step, mode, len_lo, len_hi, threads)
+    else:
+        rc = lib().oracle_synth_batch(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, base_off, stride, seed,
+                                      first, step, mode, len_lo, len_hi)
     if rc != 0:
         raise ValueError("oracle_synth_batch: frames do not fit the UMEM")
     return descs

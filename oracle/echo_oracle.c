@@ -251,7 +251,10 @@ uint32_t oracle_synth_frame(uint64_t seed, uint64_t gidx, int mode, uint32_t len
     if (s == 18) L = k_short_lens[(r5 >> 40) % 13];
     const uint32_t W = ((L > 64 ? L : 64) + 15u) & ~15u; /* fill extent: whole 16-B blocks */
     if (W > cap) return 0xFFFFFFFFu;
-    for (uint32_t o = 0; o < W; o++) out[o] = byte_of(oracle_mix64(K + 16 + (o >> 3)), (int)(o & 7));
+    for (uint32_t o = 0; o < W; o += 8) { /* W is a multiple of 16 */
+        const uint64_t v = oracle_mix64(K + 16 + (o >> 3));
+        for (int i = 0; i < 8; i++) out[o + (uint32_t)i] = byte_of(v, i);
+    }
     if (s == 19) return L; /* garbage frame: fill pattern only */
     uint8_t* p = out;
     for (int i = 0; i < 6; i++) p[i] = byte_of(r1, i);
@@ -298,6 +301,57 @@ int oracle_synth_batch(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc* d
         descs[j].options = 0;
     }
     return 0;
+}
+
+/* oracle_synth_batch over `threads` pthreads (contiguous frame ranges; same bytes). */
+struct synth_job {
+    uint8_t* umem;
+    uint64_t umem_size;
+    struct xsk_gpu_desc* descs;
+    uint32_t j0, n;
+    uint64_t base_off, stride, seed, first, step;
+    int mode;
+    uint32_t len_lo, len_hi;
+    int rc;
+};
+
+static void* synth_worker(void* arg) {
+    struct synth_job* j = (struct synth_job*)arg;
+    j->rc = oracle_synth_batch(j->umem, j->umem_size, j->descs + j->j0, j->n, j->base_off + (uint64_t)j->j0 * j->stride,
+                               j->stride, j->seed, j->first + (uint64_t)j->j0 * j->step, j->step, j->mode, j->len_lo,
+                               j->len_hi);
+    return NULL;
+}
+
+int oracle_synth_batch_mt(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc* descs, uint32_t n, uint64_t base_off,
+                          uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode, uint32_t len_lo,
+                          uint32_t len_hi, int threads) {
+    if (threads < 1) threads = 1;
+    if ((uint32_t)threads > n) threads = n ? (int)n : 1;
+    struct synth_job* jobs = (struct synth_job*)calloc((size_t)threads, sizeof *jobs);
+    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof *tids);
+    if (!jobs || !tids) {
+        free(jobs);
+        free(tids);
+        return -1;
+    }
+    uint32_t start = 0;
+    for (int t = 0; t < threads; t++) {
+        const uint32_t cnt = n / threads + ((uint32_t)t < n % threads ? 1 : 0);
+        struct synth_job jb = {umem, umem_size, descs, start, cnt, base_off, stride, seed, first, step, mode, len_lo,
+                               len_hi, 0};
+        jobs[t] = jb;
+        start += cnt;
+        if (t > 0) pthread_create(&tids[t], NULL, synth_worker, &jobs[t]);
+    }
+    synth_worker(&jobs[0]);
+    int rc = 0;
+    for (int t = 1; t < threads; t++) pthread_join(tids[t], NULL);
+    for (int t = 0; t < threads; t++)
+        if (jobs[t].rc) rc = jobs[t].rc;
+    free(jobs);
+    free(tids);
+    return rc;
 }
 
 /* Undo one echo transform on TX_REPLY frames: swap back and csum_replace2(csum, 0, 8). */

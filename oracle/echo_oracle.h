@@ -59,6 +59,9 @@ uint32_t oracle_synth_frame(uint64_t seed, uint64_t gidx, int mode, uint32_t len
 int oracle_synth_batch(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc* descs, uint32_t n, uint64_t base_off,
                        uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode, uint32_t len_lo,
                        uint32_t len_hi);
+int oracle_synth_batch_mt(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc* descs, uint32_t n, uint64_t base_off,
+                          uint64_t stride, uint64_t seed, uint64_t first, uint64_t step, int mode, uint32_t len_lo,
+                          uint32_t len_hi, int threads);
 
 /* Re-arm (bit-identical to xsk_gpu_rearm_dev). */
 void oracle_rearm(uint8_t* umem, const struct xsk_gpu_desc* descs, const uint8_t* verdicts, uint32_t n);

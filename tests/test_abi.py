@@ -137,3 +137,43 @@ def test_kernels_are_gfx950_code_objects():
     blob = open(X.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
     assert b"amdgcn-amd-amdhsa--gfx942" not in blob and b"amdgcn-amd-amdhsa--gfx90a" not in blob
+
+
+def test_tuning_code_is_not_in_the_product_library():
+    """Kernel variants and tuning switches live in libxsknet_amd_tune.so only (loaded by tests/tools)."""
+    import xsknet_amd as X
+    prod = subprocess.run(["nm", "-D", "--defined-only", X.LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout
+    for sym in ("xsk_gpu__echo_variant", "xsk_gpu__echo_wire_variant", "xsk_gpu__set_stats_atomic",
+                "xsk_gpu__set_wire_impl", "echo_wire_kernel", "echo_kernel5", "echo_kernel7"):
+        assert sym not in prod, sym
+    # the product exports the C ABI, plus one internal helper the tuning library links against
+    exported = set(re.findall(r"\bT (\w+)", prod))
+    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu"}, exported - set(declared_functions())
+    tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout
+    assert "xsk_gpu__echo_variant" in tune and "xsk_gpu__echo_wire_variant" in tune
+    L = X.tune_lib()
+    assert hasattr(L, "xsk_gpu__echo_variant")
+
+
+def test_multi_and_lowlat_validation_without_gpu():
+    """Argument checks of the multi-context API and the LOWLAT mode constant (no device calls)."""
+    import xsknet_amd as X
+    L = X.lib()
+    EINVAL = -errno.EINVAL
+    h = C.c_void_p()
+    buf = np.zeros(64, np.uint8)
+    devs = (C.c_int * 1)(0)
+    assert L.xsk_gpu_multi_init(C.byref(h), None, 1, buf.ctypes.data, 64, 64, 0) == EINVAL
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 17, buf.ctypes.data, 64, 64, 0) == EINVAL
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data + 1, 64, 64, 0) == EINVAL
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data, 64, 0, 0) == EINVAL
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data, 64, 64, 3) == EINVAL
+    assert L.xsk_gpu_init(C.byref(h), 0, buf.ctypes.data, 64, 64, 3) == EINVAL
+    assert L.xsk_gpu_multi_process(None, None, 0, None, None, None) == EINVAL
+    assert L.xsk_gpu_multi_set_options(None, 1) == EINVAL
+    L.xsk_gpu_multi_fini(None)
+    hdr = open(HEADER).read()
+    assert "XSK_GPU_MODE_LOWLAT = 2" in hdr and f"XSK_GPU_LOWLAT_MAX {X.LOWLAT_MAX}u" in hdr
+    assert f"XSK_GPU_MULTI_MAX {X.MULTI_MAX}" in hdr

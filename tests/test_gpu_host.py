@@ -1,0 +1,179 @@
+"""Host-UMEM paths on the GPU, bit for bit against the CPU oracle: BASELINE config 1's exact workload
+(4096 x 64-B frames in one 16 MiB UMEM of 4 KiB chunks, RX_BATCH_SIZE batches -- src/lib/xsk_utils.h:6-8,
+src/lib/xsk_receive.c:220-233) in every host mode, the low-latency doorbell mode (resident polling kernel),
+and the multi-context path (several contexts over ONE UMEM, descriptor i on context i mod G)."""
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import xsknet_amd as X  # noqa: E402
+
+COUNTERS = ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")
+MODES = [X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT]
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def run_batches(ctx, descs, batch, want_recs=True):
+    tot = {k: 0 for k in COUNTERS}
+    vs, rs = [], []
+    for i in range(0, len(descs), batch):
+        v, r, s = ctx.process(descs[i:i + batch], want_recs=want_recs)
+        vs.append(v)
+        rs.append(r)
+        for k in tot:
+            tot[k] += int(s[k])
+    return np.concatenate(vs), (np.concatenate(rs) if want_recs else None), tot
+
+
+def check(umem, work, descs, v, r, tot):
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    assert (v == v_ref).all(), np.nonzero(v != v_ref)[0][:8]
+    if r is not None:
+        assert (r == r_ref).all(), np.nonzero(r != r_ref)[0][:8]
+    for k in COUNTERS:
+        assert tot[k] == int(s_ref[k]), k
+    diff = np.nonzero(work != ref)[0]
+    assert len(diff) == 0, f"{len(diff)} bytes differ, first at {diff[:8]}"
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c1_exact_workload(mode):
+    """BASELINE config 1: 4096 x 64-B ICMP echo requests, one per 4 KiB chunk at the 256-B AF_XDP headroom,
+    in RX_BATCH_SIZE (64) batches -- every frame replied, every byte as process_packet() leaves it."""
+    _dev()
+    n = 4096
+    umem = np.zeros(4096 * 4096, np.uint8)
+    descs = oracle.synth_batch(umem, n, 256, 4096, seed=0x5EED0001, mode=0, len_lo=64, len_hi=64)
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=64, mode=mode) as ctx:
+        v, r, tot = run_batches(ctx, descs, 64)
+    check(umem, work, descs, v, r, tot)
+    assert (v == X.TX_REPLY).all() and tot["tx_packets"] == n and tot["tx_bytes"] == 64 * n
+
+
+@pytest.mark.parametrize("batch", [1, 64, 1000, 1024])
+def test_lowlat_mixed_batches(batch):
+    """The doorbell path over mixed traffic (every negative / edge case) at odd batch sizes up to the
+    doorbell's 1024 frames, records on and off."""
+    _dev()
+    n = 5000
+    umem = np.zeros(n * 2048 + 4096, np.uint8)
+    descs = oracle.synth_batch(umem, n, 256, 2048, seed=0x5EED1C1C + batch, mode=1, len_lo=20, len_hi=1900)
+    for want in (True, False):
+        work = umem.copy()
+        with X.EchoContext(work, 0, max_batch=max(batch, 1), mode=X.MODE_LOWLAT) as ctx:
+            v, r, tot = run_batches(ctx, descs, batch, want_recs=want)
+        check(umem, work, descs, v, r, tot)
+
+
+def test_lowlat_idle_exit_large_batches_and_options():
+    """The resident kernel leaves after 50 ms without a batch and the next call brings it back; a batch
+    above the doorbell's size stops it and takes the launch path; switching to wire-format options
+    restarts it in wire mode -- results exact throughout, frames recycled between calls."""
+    _dev()
+    n = 3 * 1024 + 2048 + 512
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED1D1D, mode=1, len_lo=20, len_hi=1500)
+    work = umem.copy()
+    parts = [(0, 64), (64, 1024), (1088, 2048), (3136, 1000), (4136, 512), (4648, n - 4648)]
+    tot = {k: 0 for k in COUNTERS}
+    vs = []
+    with X.EchoContext(work, 0, max_batch=2048, mode=X.MODE_LOWLAT) as ctx:
+        for i, (a, m) in enumerate(parts):
+            if i == 3:
+                time.sleep(0.12)  # > 50 ms idle: the kernel exits on its own
+            v, _, s = ctx.process(descs[a:a + m], want_recs=False)
+            vs.append(v)
+            for k in tot:
+                tot[k] += int(s[k])
+    check(umem, work, descs, np.concatenate(vs), None, tot)
+    # wire mode through the doorbell (the spec oracle: oracle_echo_batch_opts)
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
+        v0, _, _ = ctx.process(descs[:64], want_recs=False)
+        ctx.set_options(X.OPT_ALL)
+        v1, r1, _ = ctx.process(descs[64:1088])
+    ref = umem.copy()
+    v_ref0, _, _ = oracle.echo_batch_opts(ref, descs[:64], 0)
+    v_ref1, r_ref1, _ = oracle.echo_batch_opts(ref, descs[64:1088], X.OPT_ALL)
+    assert (v0 == v_ref0).all() and (v1 == v_ref1).all() and (r1 == r_ref1).all()
+    assert (work == ref).all()
+
+
+def test_lowlat_many_small_calls():
+    """20 000 back-to-back 64-frame doorbell calls over a recycled 4096-frame UMEM (the RX loop's steady
+    state): the polling kernel must see every new frame, never a stale cached one."""
+    _dev()
+    n, batch, passes = 4096, 64, 5
+    umem = np.zeros(n * 4096, np.uint8)
+    descs = oracle.synth_batch(umem, n, 256, 4096, seed=0x5EED1E1E, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    work = umem.copy()
+    t = 0.0
+    with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_LOWLAT) as ctx:
+        for p in range(passes):
+            work[:] = umem  # the frames are recycled: new requests at the same UMEM addresses
+            t0 = time.perf_counter()
+            v, r, tot = run_batches(ctx, descs, batch)
+            t += time.perf_counter() - t0
+            assert (v == v_ref).all() and (r == r_ref).all(), p
+            for k in COUNTERS:
+                assert tot[k] == int(s_ref[k])
+            assert (work == ref).all(), p
+    print(f"lowlat: {t / (passes * n // batch) * 1e6:.1f} us per 64-frame call (Python driver)")
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_context_one_gpu(mode, devices):
+    """G contexts on device 0 over ONE registered UMEM (the rehearsal of G GPUs): descriptor i on context
+    i mod G, each on its own host thread and stream; verdicts, records and every byte exact, counters summed."""
+    _dev()
+    n = 20000
+    umem = np.zeros(n * 2048 + 256, np.uint8)
+    descs = oracle.synth_batch(umem, n, 256, 2048, seed=0x5EED2020 + len(devices), mode=1, len_lo=20, len_hi=1500)
+    for batch in (64, 3001, n):
+        work = umem.copy()
+        with X.MultiContext(work, devices, max_batch=batch, mode=mode) as m:
+            v, r, tot = run_batches(m, descs, batch)
+        check(umem, work, descs, v, r, tot)
+
+
+def test_multi_context_wire_options():
+    _dev()
+    n = 4000
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2121, mode=1, len_lo=20, len_hi=1500)
+    work = umem.copy()
+    with X.MultiContext(work, [0, 0], max_batch=n, mode=X.MODE_STAGED, opts=X.OPT_ALL) as m:
+        v, r, _ = m.process(descs)
+    ref = umem.copy()
+    v_ref, r_ref, _ = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
+    assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
+
+
+def test_multi_context_argument_checks():
+    import ctypes as C
+    import errno
+    L = X.lib()
+    buf = np.zeros(4096, np.uint8)
+    h = C.c_void_p()
+    devs = (C.c_int * 2)(0, 0)
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 0, buf.ctypes.data, buf.nbytes, 64, 0) == -errno.EINVAL
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 2, buf.ctypes.data, buf.nbytes, 64, 9) == -errno.EINVAL
+    bad = (C.c_int * 2)(0, 999)
+    assert L.xsk_gpu_multi_init(C.byref(h), bad, 2, buf.ctypes.data, buf.nbytes, 64, 0) == -errno.ENODEV
+    assert L.xsk_gpu_multi_process(None, None, 0, None, None, None) == -errno.EINVAL
+    L.xsk_gpu_multi_fini(None)

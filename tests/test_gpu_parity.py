@@ -1,8 +1,8 @@
 """GPU parity: the gfx950 kernels (through the C ABI) vs the CPU oracle, bit for bit.
 
-Everything here runs on a real MI355X (``-m gpu``).  Small cases compare every byte of the UMEM,
-every verdict, record and counter with ``oracle/``; full-size cases (BASELINE configs at 1 M frames)
-use size-independent properties plus sampled per-frame oracle checks.
+Everything here runs on a real MI355X (``-m gpu``).  Every case compares every byte of the UMEM, every
+verdict, record and counter with ``oracle/`` -- the full-size BASELINE configs too (c2/c3/c4 at 1 M
+frames, C5's 8 M-frame per-GPU shard), plus the re-arm round trip.
 """
 import os
 import subprocess
@@ -221,15 +221,11 @@ def test_stats_accumulate_across_calls():
     assert (d_umem.cpu().numpy() == ref).all()
 
 
-@pytest.mark.parametrize("atomic", [1, 0])
-def test_counter_delivery_modes(atomic):
-    """Both counter deliveries (device atomics, shipped; partials + fold launch) accumulate the oracle's
-    counters over many workgroups, on top of what the stats already hold, and leave `timestamp` alone."""
-    import ctypes as C
+def test_counters_device_atomics():
+    """Every workgroup adds its counters to the caller's stats with device-scope atomics, on top of what
+    they already hold, leaving `timestamp` alone (many workgroups plus a ragged tail)."""
     dev = _dev()
-    L = X.lib()
-    L.xsk_gpu__set_stats_atomic.argtypes = [C.c_int]
-    n = 300_000  # tiles for every workgroup of a 256-CU grid, plus a ragged tail
+    n = 300_000
     umem = np.zeros(n * 2048, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=77, mode=1, len_lo=0, len_hi=1500)
     ref = umem.copy()
@@ -240,12 +236,8 @@ def test_counter_delivery_modes(atomic):
     base["tx_packets"], base["tx_bytes"] = 7, 11
     d_stats = to_dev(base)
     ws = torch.zeros(X.workspace_size(0, n), dtype=torch.uint8, device=dev)
-    assert L.xsk_gpu__set_stats_atomic(atomic) == 0
-    try:
-        X.echo_dev(d_umem, d_descs, n, None, None, d_stats, ws)
-        torch.cuda.synchronize()
-    finally:
-        L.xsk_gpu__set_stats_atomic(1)
+    X.echo_dev(d_umem, d_descs, n, None, None, d_stats, ws)
+    torch.cuda.synchronize()
     s = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
     for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
         assert int(s[k]) == int(s_ref[k]) + int(base[k][0]), k
@@ -253,7 +245,30 @@ def test_counter_delivery_modes(atomic):
     assert (d_umem.cpu().numpy() == ref).all()
 
 
-@pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED])
+def test_small_batches_share_stats_across_streams():
+    """One-workgroup calls (RX_BATCH_SIZE frames) on four streams at once, all adding into ONE device
+    stats_record: the counts are exact (device atomics, never a plain read-modify-write)."""
+    dev = _dev()
+    n, calls = 64, 400
+    umem = np.zeros(n * calls * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n * calls, 0, 2048, seed=0x5EED5151, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    _, _, s_ref = oracle.echo_batch(ref, descs)
+    d_umem, d_descs = to_dev(umem), to_dev(descs)
+    d_stats = torch.zeros(40, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(X.workspace_size(0, n), dtype=torch.uint8, device=dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    torch.cuda.synchronize()
+    for c in range(calls):
+        X.echo_dev(d_umem, d_descs[c * n * 16:(c + 1) * n * 16], n, None, None, d_stats, ws, stream=streams[c % 4])
+    torch.cuda.synchronize()
+    s = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        assert int(s[k]) == int(s_ref[k]), k
+    assert (d_umem.cpu().numpy() == ref).all()
+
+
+@pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT])
 def test_host_umem_modes(mode):
     """C1 shape: 4096 frames in a 16 MiB UMEM of 4 KiB chunks, RX batches of 64 (and one big batch)."""
     n = 4096
@@ -293,9 +308,10 @@ def test_echo_replay_tool():
         p = lambda s: os.path.join(td, s)  # noqa: E731
         umem.tofile(p("u"))
         descs.tofile(p("d"))
-        for mode in ("zerocopy", "staged"):
-            r = subprocess.run([exe, p("u"), p("d"), p("o"), p("v"), "64", mode], capture_output=True, text=True,
-                               timeout=300)
+        for mode, extra in (("zerocopy", []), ("staged", []), ("lowlat", []), ("lowlat", ["reps=3"]),
+                            ("zerocopy", ["gpus=0,0"]), ("staged", ["gpus=0,0,0", "reps=2"])):
+            r = subprocess.run([exe, p("u"), p("d"), p("o"), p("v"), "64", mode] + extra, capture_output=True,
+                               text=True, timeout=300)
             assert r.returncode == 0, r.stderr
             kv = dict(x.split("=") for x in r.stdout.split())
             assert int(kv["rx_packets"]) == int(s_ref["rx_packets"])
@@ -320,50 +336,82 @@ def test_rearm_gpu_roundtrip():
     assert torch.equal(before, d_umem)
 
 
-@pytest.mark.parametrize("cfg", ["c2_64", "c3_1500", "c4_mixed"])
-def test_full_size_configs(cfg):
-    """BASELINE configs 2-4 at full size (1 M frames): properties + sampled oracle checks."""
+def _threads():
+    return min(16, oracle.cpu_threads())
+
+
+def full_batch_parity(n, lo, hi, stride, seed, first=0, step=1, mode=0, chunk=1 << 20):
+    """Generate n frames on the GPU, transform them with ONE xsk_gpu_echo_dev call, and compare every
+    byte of the slab, every verdict, record and counter with the oracle run on a host image regenerated
+    by oracle.synth_batch (chunk by chunk, so host memory stays bounded); then the rearm round trip."""
     dev = _dev()
-    n = 1 << 20
-    lo, hi, stride = {"c2_64": (64, 64, 64), "c3_1500": (1500, 1500, 4096), "c4_mixed": (64, 1500, 2048)}[cfg]
-    seed = 0x5EED0000 + {"c2_64": 2, "c3_1500": 3, "c4_mixed": 4}[cfg]
     d_umem = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
     d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    X.synth_dev(d_umem, d_descs, n, 0, stride, seed, 0, 1, 0, lo, hi)
-    before = d_umem.clone()
-    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    X.synth_dev(d_umem, d_descs, n, 0, stride, seed, first, step, mode, lo, hi)
+    d_verd = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
     d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     d_stats = torch.zeros(40, dtype=torch.uint8, device=dev)
     ws = torch.zeros(X.workspace_size(0, n), dtype=torch.uint8, device=dev)
     X.echo_dev(d_umem, d_descs, n, d_verd, d_recs, d_stats, ws)
     torch.cuda.synchronize()
-    descs = d_descs.cpu().numpy().view(X.DESC_DTYPE)
+    tot = {k: 0 for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")}
+    verdicts = d_verd.cpu().numpy()
     recs = d_recs.cpu().numpy().view(X.REC_DTYPE)
-    stats = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
-    # properties: every generated request is accepted and its IP/ICMP checksums verify
-    assert (d_verd.cpu().numpy() == 0).all()
-    assert (recs["flags"] == 3).all()
-    assert int(stats["rx_packets"]) == n and int(stats["tx_packets"]) == n
-    assert int(stats["rx_bytes"]) == int(descs["len"].sum()) == int(stats["tx_bytes"])
-    # the reply checksum makes the reply verify too: sum(reply ICMP) == 0xFFFF  <=>  recompute == out
-    # sampled frames: regenerate on the CPU and compare bytes with the oracle's transform
-    rng = np.random.default_rng(0)
-    idx = np.sort(rng.choice(n, 512, replace=False))
-    got = d_umem.view(-1, stride)[torch.from_numpy(idx).to(dev)].cpu().numpy()
-    for k, j in enumerate(idx):
-        L, buf = oracle.synth_frame(seed, int(j), 0, lo, hi, cap=max(stride, 64))
-        assert L == descs[j]["len"]
-        frame = buf[:stride].copy()
-        d1 = np.zeros(1, oracle.DESC_DTYPE)
-        d1[0] = (0, L, 0)
-        v, r, _ = oracle.echo_batch(frame, d1)
-        assert v[0] == 0
-        assert (got[k] == frame).all(), j
-        assert r[0] == recs[j]
-    # round trip: rearm restores the exact input slab
-    X.rearm_dev(d_umem, d_descs, d_verd, n)
-    torch.cuda.synchronize()
-    assert torch.equal(before, d_umem)
+    descs_all = d_descs.cpu().numpy().view(X.DESC_DTYPE)
+    th = _threads()
+    for j0 in range(0, n, chunk):
+        m = min(chunk, n - j0)
+        host = np.zeros(m * stride, np.uint8)
+        descs = oracle.synth_batch(host, m, 0, stride, seed, first + j0 * step, step, mode, lo, hi, threads=th)
+        assert (descs["len"] == descs_all["len"][j0:j0 + m]).all()
+        v_ref, r_ref, s_ref = oracle.echo_batch(host, descs, threads=th)
+        got = d_umem[j0 * stride:(j0 + m) * stride].cpu().numpy()
+        diff = np.nonzero(got != host)[0]
+        assert len(diff) == 0, f"frames from {j0}: {len(diff)} bytes differ, first at {diff[:8]}"
+        assert (verdicts[j0:j0 + m] == v_ref).all()
+        bad = np.nonzero(recs[j0:j0 + m] != r_ref)[0]
+        assert len(bad) == 0, (j0 + bad[:5])
+        for k in tot:
+            tot[k] += int(s_ref[k])
+        del host, got
+    st = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    for k in tot:
+        assert int(st[k]) == tot[k], k
+    # round trip: re-arm restores the exact generated input (valid requests only, mode 0)
+    if mode == 0:
+        before = torch.zeros_like(d_umem)
+        X.synth_dev(before, d_descs, n, 0, stride, seed, first, step, mode, lo, hi)
+        X.rearm_dev(d_umem, d_descs, d_verd, n)
+        torch.cuda.synchronize()
+        assert torch.equal(before, d_umem)
+    return verdicts
+
+
+@pytest.mark.parametrize("cfg", ["c2_64", "c3_1500", "c4_mixed"])
+def test_full_size_configs(cfg):
+    """BASELINE configs 2-4 at full size (1 M frames, one call): every frame byte-exact vs the oracle."""
+    lo, hi, stride = {"c2_64": (64, 64, 64), "c3_1500": (1500, 1500, 4096), "c4_mixed": (64, 1500, 2048)}[cfg]
+    seed = 0x5EED0000 + {"c2_64": 2, "c3_1500": 3, "c4_mixed": 4}[cfg]
+    v = full_batch_parity(1 << 20, lo, hi, stride, seed)
+    assert (v == 0).all()
+
+
+def test_full_size_mixed_traffic():
+    """1 M frames of every negative / edge case (mode 1) at a 2 KiB stride, every frame vs the oracle."""
+    full_batch_parity(1 << 20, 20, 1500, 2048, 0x5EED0044, mode=1)
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c5_shard(rank):
+    """BASELINE config 5 at 8 GPUs: this rank's shard of the 64 M x 1500 B step -- 8 M frames, global
+    frame first + j * 8 (round-robin, bench.py / shard.py), 2 KiB stride (16 GiB of UMEM) -- in ONE
+    call, every byte of every frame vs the oracle."""
+    from xsknet_amd import shard
+    world = 8
+    n = (1 << 26) // world
+    first, step = shard.shard_range(0, n, rank, world)
+    v = full_batch_parity(n, 1500, 1500, 2048, 0x5EED0005, first=first, step=step, chunk=1 << 21)
+    assert (v == 0).all()
 
 
 def test_timing_hook():
@@ -387,10 +435,7 @@ def test_kernel_variants_parity(variant, grid, len_hi):
     """Every ring depth / grid shape the tuning sweep may select is bit-exact (multi-tile waves too);
     len_hi 112 makes tiles of ping-size frames (every frame within 128 B of its 16-B aligned start), 48
     tiles whose frames all fit their 64-B windows."""
-    import ctypes as C
-    L = X.lib()
-    L.xsk_gpu__echo_variant.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
-                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L = X.tune_lib()
     dev = _dev()
     n, stride = 3000, 2048 + 16
     umem = np.zeros(n * stride + 64, np.uint8)

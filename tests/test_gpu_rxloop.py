@@ -55,8 +55,12 @@ def _dev():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED])
-def test_rx_loop_end_to_end(mode):
+@pytest.mark.parametrize("mode,ctx_batch,step_batch", [(X.MODE_ZEROCOPY, 1024, 64), (X.MODE_STAGED, 1024, 64),
+                                                      (X.MODE_LOWLAT, 1024, 64), (X.MODE_LOWLAT, 64, 1024),
+                                                      (X.MODE_ZEROCOPY, 64, 1024)])
+def test_rx_loop_end_to_end(mode, ctx_batch, step_batch):
+    """ctx_batch < step_batch: the step peeks no more than the context takes (never an -EINVAL after the
+    fill ring was restocked)."""
     _dev()
     n_pkts, seed = 20000, 0x5EED0A0A
     umem = np.zeros(NUM_FRAMES * FRAME_SIZE, np.uint8)
@@ -77,7 +81,7 @@ def test_rx_loop_end_to_end(mode):
     sent = 0
     replies_seen = 0
     delivered = collections.deque()  # RX order
-    with X.EchoContext(umem, 0, max_batch=1024, mode=mode) as ctx:
+    with X.EchoContext(umem, 0, max_batch=ctx_batch, mode=mode) as ctx:
         guard = 0
         while sent < n_pkts or rx.k_avail():
             guard += 1
@@ -104,7 +108,8 @@ def test_rx_loop_end_to_end(mode):
             if descs:
                 rx.k_push(np.array(descs, X.DESC_DTYPE))
             # app: one RX loop step (batches of 64 like RX_BATCH_SIZE), then completions
-            got, res = ctx.rx_step(rx.view, fq.view, tx.view, pool, 64, totals)
+            got, res = ctx.rx_step(rx.view, fq.view, tx.view, pool, step_batch, totals)
+            assert got <= min(ctx_batch, step_batch)
             assert res.tx_full == 0
             # kernel: transmit -> check bytes -> complete
             txd = tx.k_pop(tx.k_avail())

@@ -3,7 +3,14 @@
  * batch, the way the reference client's RX loop does (src/lib/xsk_receive.c:192-237), with the
  * per-descriptor process_packet() call replaced by one xsk_gpu_process() per batch.
  *
- *   echo_replay <umem.bin> <descs.bin> <out_umem.bin> <out_verdicts.bin> [batch] [zerocopy|staged]
+ *   echo_replay <umem.bin> <descs.bin> <out_umem.bin> <out_verdicts.bin> [batch] [zerocopy|staged|lowlat]
+ *               [gpus=D0,D1,...] [reps=R]
+ *
+ * With gpus=..., the batches go through xsk_gpu_multi_process() over one context per listed device
+ * (repeats allowed): descriptor i of a batch on context i mod G, counters summed on the host.
+ * With reps=R (R >= 1), the replay is timed: R passes over the image, the UMEM restored from the input
+ * between passes (untimed), and one more key=value pair, us_per_call (wall clock per batch call, the
+ * first pass -- which starts the device side -- excluded), is printed; the outputs are those of pass 1.
  *
  * umem.bin: raw UMEM bytes (size multiple of 16).  descs.bin: packed struct xdp_desc records
  * (u64 addr, u32 len, u32 options).  Prints the stats_record counters the reference's stats
@@ -14,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../include/xsk_gpu.h"
 
@@ -50,12 +58,29 @@ static int dump(const char* path, const void* p, size_t n) {
 
 int main(int argc, char** argv) {
     if (argc < 5) {
-        fprintf(stderr, "usage: %s umem.bin descs.bin out_umem.bin out_verdicts.bin [batch] [zerocopy|staged]\n",
+        fprintf(stderr,
+                "usage: %s umem.bin descs.bin out_umem.bin out_verdicts.bin [batch] [zerocopy|staged|lowlat] "
+                "[gpus=D0,D1,...]\n",
                 argv[0]);
         return 2;
     }
     const uint32_t batch = argc > 5 ? (uint32_t)strtoul(argv[5], NULL, 10) : RX_BATCH_SIZE;
-    const int mode = (argc > 6 && strcmp(argv[6], "staged") == 0) ? XSK_GPU_MODE_STAGED : XSK_GPU_MODE_ZEROCOPY;
+    int mode = XSK_GPU_MODE_ZEROCOPY;
+    if (argc > 6 && strcmp(argv[6], "staged") == 0) mode = XSK_GPU_MODE_STAGED;
+    if (argc > 6 && strcmp(argv[6], "lowlat") == 0) mode = XSK_GPU_MODE_LOWLAT;
+    int devices[XSK_GPU_MULTI_MAX];
+    uint32_t ndev = 0, reps = 0;
+    for (int a = 7; a < argc; a++) {
+        if (strncmp(argv[a], "gpus=", 5) == 0) {
+            for (char* p = argv[a] + 5; *p && ndev < XSK_GPU_MULTI_MAX;) {
+                devices[ndev++] = (int)strtol(p, &p, 10);
+                if (*p == ',') p++;
+                else break;
+            }
+        } else if (strncmp(argv[a], "reps=", 5) == 0) {
+            reps = (uint32_t)strtoul(argv[a] + 5, NULL, 10);
+        }
+    }
     size_t umem_size = 0, desc_bytes = 0;
     /* page-aligned like the reference's posix_memalign(getpagesize(), ...) (xsk_utils.c:135) */
     uint8_t* umem = (uint8_t*)slurp(argv[1], &umem_size, 4096);
@@ -66,42 +91,78 @@ int main(int argc, char** argv) {
     }
     const uint32_t n = (uint32_t)(desc_bytes / sizeof *descs);
     uint8_t* verdicts = (uint8_t*)calloc(n ? n : 1, 1);
+    uint8_t* scratch = (uint8_t*)calloc(n ? n : 1, 1);
+    uint8_t *pristine = NULL, *out1 = NULL;
+    if (reps) {
+        pristine = (uint8_t*)malloc(umem_size ? umem_size : 1);
+        out1 = (uint8_t*)malloc(umem_size ? umem_size : 1);
+        if (!pristine || !out1) return 1;
+        memcpy(pristine, umem, umem_size);
+    }
 
     xsk_gpu_ctx* ctx = NULL;
-    int rc = xsk_gpu_init(&ctx, 0, umem, umem_size, batch, mode);
+    xsk_gpu_multi* multi = NULL;
+    int rc = ndev ? xsk_gpu_multi_init(&multi, devices, ndev, umem, umem_size, batch, mode)
+                  : xsk_gpu_init(&ctx, 0, umem, umem_size, batch, mode);
     if (rc) {
-        fprintf(stderr, "xsk_gpu_init: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
+        fprintf(stderr, "init: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
         return 1;
     }
-    struct xsk_gpu_stats stats;
+    struct xsk_gpu_stats stats, st_rep;
     memset(&stats, 0, sizeof stats);
-    uint64_t freed = 0, tx_ready = 0;
-    /* handle_receive_packets(): one RX peek of <= batch descriptors per iteration */
-    for (uint32_t i = 0; i < n; i += batch) {
-        const uint32_t rcvd = n - i < batch ? n - i : batch;
-        rc = xsk_gpu_process(ctx, descs + i, rcvd, verdicts + i, NULL, &stats);
-        if (rc) {
-            fprintf(stderr, "xsk_gpu_process: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
-            xsk_gpu_fini(ctx);
-            return 1;
+    uint64_t freed = 0, tx_ready = 0, timed_calls = 0;
+    double timed_s = 0.0;
+    const uint32_t passes = reps ? reps : 1;
+    for (uint32_t pass = 0; pass < passes; pass++) {
+        if (pass) memcpy(umem, pristine, umem_size); /* untimed: the frames are requests again */
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        /* handle_receive_packets(): one RX peek of <= batch descriptors per iteration */
+        for (uint32_t i = 0; i < n; i += batch) {
+            const uint32_t rcvd = n - i < batch ? n - i : batch;
+            rc = multi ? xsk_gpu_multi_process(multi, descs + i, rcvd, (pass ? scratch : verdicts) + i, NULL,
+                                               pass ? &st_rep : &stats)
+                       : xsk_gpu_process(ctx, descs + i, rcvd, (pass ? scratch : verdicts) + i, NULL,
+                                         pass ? &st_rep : &stats);
+            if (rc) {
+                fprintf(stderr, "process: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
+                xsk_gpu_multi_fini(multi);
+                xsk_gpu_fini(ctx);
+                return 1;
+            }
+            if (pass) continue;
+            /* the reference sendto()s TX_REPLY frames, then frees every frame (:166, :226-227) */
+            for (uint32_t k = 0; k < rcvd; k++) {
+                if (verdicts[i + k] == XSK_GPU_TX_REPLY) tx_ready++;
+                freed++;
+            }
         }
-        /* the reference sendto()s TX_REPLY frames, then frees every frame (:166, :226-227) */
-        for (uint32_t k = 0; k < rcvd; k++) {
-            if (verdicts[i + k] == XSK_GPU_TX_REPLY) tx_ready++;
-            freed++;
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (pass == 0 && reps) memcpy(out1, umem, umem_size);
+        if (pass > 0) {
+            timed_s += (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+            timed_calls += (n + batch - 1) / batch;
         }
     }
+    if (reps) memcpy(umem, out1, umem_size);
+    xsk_gpu_multi_fini(multi);
     xsk_gpu_fini(ctx);
     if (dump(argv[3], umem, umem_size) || dump(argv[4], verdicts, n)) {
         fprintf(stderr, "cannot write outputs\n");
         return 1;
     }
-    printf("rx_packets=%llu rx_bytes=%llu tx_packets=%llu tx_bytes=%llu freed=%llu tx_ready=%llu\n",
+    printf("rx_packets=%llu rx_bytes=%llu tx_packets=%llu tx_bytes=%llu freed=%llu tx_ready=%llu",
            (unsigned long long)stats.rx_packets, (unsigned long long)stats.rx_bytes,
            (unsigned long long)stats.tx_packets, (unsigned long long)stats.tx_bytes, (unsigned long long)freed,
            (unsigned long long)tx_ready);
+    if (timed_calls) printf(" us_per_call=%.3f calls=%llu", timed_s / (double)timed_calls * 1e6,
+                            (unsigned long long)timed_calls);
+    printf("\n");
     free(umem);
     free(descs);
     free(verdicts);
+    free(scratch);
+    free(pristine);
+    free(out1);
     return 0;
 }

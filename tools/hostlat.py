@@ -1,42 +1,59 @@
 #!/usr/bin/env python3
-"""Per-call latency of the host-UMEM drop-in (xsk_gpu_process) at RX-loop batch sizes: the C1 shape
-(4096 x 64-B frames in a 16 MiB UMEM of 4 KiB chunks, 256-B headroom) processed in batches of
-64 (RX_BATCH_SIZE, xsk_utils.h:8) up to 4096 frames, zerocopy and staged.  Prints one JSON line per
-(mode, batch): microseconds per call and Mframes/s.  Frames are re-armed (untimed) between passes."""
+"""Per-call latency of the host-UMEM drop-in at RX-loop batch sizes, timed in C (tools/echo_replay reps=R).
+
+The C1 shape: 4096 frames in a 16 MiB UMEM of 4 KiB chunks at a 256-B headroom (xsk_utils.h:6-7), processed
+in batches of 64 (RX_BATCH_SIZE, xsk_utils.h:8) up to 4096 frames, for the zerocopy, staged and low-latency
+(resident polling kernel) modes, and the multi-context path (``--gpus 0,0``).  Each timed pass restores the
+UMEM (untimed) so every call transforms echo requests.  Prints one JSON line per (frame length, mode, batch).
+
+  python tools/hostlat.py [--lens 64,1500] [--modes zerocopy,staged,lowlat] [--batches 64,256,1024,4096]
+                          [--gpus 0,0] [--reps 200]
+"""
+import argparse
 import json
 import os
+import subprocess
 import sys
-import time
+import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
-import oracle  # noqa: E402  (frame generator + re-arm only)
-import xsknet_amd as X  # noqa: E402
+import oracle  # noqa: E402  (frame generator only)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lens", default="64,1500")
+    ap.add_argument("--modes", default="zerocopy,staged,lowlat")
+    ap.add_argument("--batches", default="64,256,1024,4096")
+    ap.add_argument("--gpus", default="")
+    ap.add_argument("--reps", type=int, default=100)
+    args = ap.parse_args()
+    exe = os.path.join(ROOT, "tools", "echo_replay")
     n, chunk = 4096, 4096
-    for flen in (64, 1500):
-        umem = np.zeros(n * chunk, np.uint8)
-        descs = oracle.synth_batch(umem, n, 256, chunk, seed=0x5EED0001, mode=0, len_lo=flen, len_hi=flen)
-        for name, mode in (("zerocopy", X.MODE_ZEROCOPY), ("staged", X.MODE_STAGED)):
-            for batch in (64, 256, 1024, 4096):
-                with X.EchoContext(umem, 0, max_batch=batch, mode=mode) as ctx:
-                    for i in range(0, n, batch):  # warm
-                        ctx.process(descs[i:i + batch], want_recs=False)
-                    oracle.rearm(umem, descs, np.zeros(n, np.uint8))
-                    calls, t = 0, 0.0
-                    while t < 1.0:
-                        t0 = time.perf_counter()
-                        for i in range(0, n, batch):
-                            ctx.process(descs[i:i + batch], want_recs=False)
-                        t += time.perf_counter() - t0
-                        calls += n // batch
-                        oracle.rearm(umem, descs, np.zeros(n, np.uint8))
-                print(json.dumps({"frame_len": flen, "mode": name, "batch": batch, "us_per_call": round(t / calls * 1e6, 1),
-                                  "mframes_s": round(calls * batch / t / 1e6, 3)}), flush=True)
+    with tempfile.TemporaryDirectory() as td:
+        p = lambda s: os.path.join(td, s)  # noqa: E731
+        for flen in (int(x) for x in args.lens.split(",")):
+            umem = np.zeros(n * chunk, np.uint8)
+            descs = oracle.synth_batch(umem, n, 256, chunk, seed=0x5EED0001, mode=0, len_lo=flen, len_hi=flen)
+            umem.tofile(p("u"))
+            descs.tofile(p("d"))
+            for mode in args.modes.split(","):
+                for batch in (int(x) for x in args.batches.split(",")):
+                    cmd = [exe, p("u"), p("d"), p("o"), p("v"), str(batch), mode, f"reps={args.reps}"]
+                    if args.gpus:
+                        cmd.insert(7, f"gpus={args.gpus}")
+                    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+                    if r.returncode != 0:
+                        print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "error": r.stderr[-300:]}))
+                        sys.exit(1)
+                    kv = dict(x.split("=") for x in r.stdout.split())
+                    us = float(kv["us_per_call"])
+                    print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0",
+                                      "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3),
+                                      "calls": int(kv["calls"])}), flush=True)
 
 
 if __name__ == "__main__":

@@ -11,7 +11,6 @@ same P (LITE), 50+ = the shipped row-streaming kernel at other settings, see xsk
 Prints one JSON line per (layout, variant, grid) to stdout.
 """
 import argparse
-import ctypes as C
 import json
 import os
 import sys
@@ -44,10 +43,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pool", type=int, default=1)
     args = ap.parse_args()
-    L = X.lib()
-    L.xsk_gpu__echo_variant.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
-                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
-    L.xsk_gpu__echo_variant.restype = C.c_int
+    L = X.tune_lib()
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream

@@ -2,7 +2,6 @@
 """Is the round kernel's per-XCD speed stable from launch to launch?  Runs the timing-probe variant
 (79: echo_kernel6 + per-workgroup start/end wall clock) over a pool of cold c3 batches and prints the
 per-XCD mean end time of every launch (workgroup g runs on XCD g % 8)."""
-import ctypes as C
 import json
 import os
 import sys
@@ -15,9 +14,7 @@ import xsknet_amd as X  # noqa: E402
 
 
 def main():
-    L = X.lib()
-    L.xsk_gpu__echo_variant.argtypes = [C.c_int, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
-                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L = X.tune_lib()
     n, stride, pool = 1 << 20, 4096, 8
     dev = torch.device("cuda:0")
     umems, descs = [], []

@@ -22,7 +22,7 @@ __all__ = [
     "LIB_PATH", "lib", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
-    "MODE_ZEROCOPY", "MODE_STAGED", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
+    "MODE_ZEROCOPY", "MODE_STAGED", "MODE_LOWLAT", "LOWLAT_MAX", "MultiContext", "tune_lib", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
     "classify_dev", "XDP_DROP", "XDP_PASS", "XDP_REDIRECT", "DROP_BAD_IP", "DROP_BAD_CSUM",
     "OPT_STRICT_IPV4", "OPT_VLAN", "OPT_VERIFY_CSUM", "OPT_ALL", "F_IP_CSUM_OK", "F_ICMP_CSUM_OK", "F_VLAN",
     "F_IP_OPTIONS",
@@ -30,6 +30,8 @@ __all__ = [
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxsknet_amd.so")
+# kernel variants for the tuning sweep (tools/kbench.py) and their parity tests; never the product path
+TUNE_LIB_PATH = os.path.join(_HERE, "libxsknet_amd_tune.so")
 
 TX_REPLY, DROP_SHORT, DROP_NOT_IPV4, DROP_NOT_ICMP, DROP_NOT_ECHO, DROP_BAD_DESC, DROP_BAD_IP, DROP_BAD_CSUM = range(8)
 VERDICTS = ["TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
@@ -37,7 +39,9 @@ VERDICTS = ["TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NO
 # wire-format options (include/xsk_gpu.h XSK_GPU_OPT_*) and record flags
 OPT_STRICT_IPV4, OPT_VLAN, OPT_VERIFY_CSUM, OPT_ALL = 1, 2, 4, 7
 F_IP_CSUM_OK, F_ICMP_CSUM_OK, F_VLAN, F_IP_OPTIONS = 1, 2, 4, 8
-MODE_ZEROCOPY, MODE_STAGED = 0, 1
+MODE_ZEROCOPY, MODE_STAGED, MODE_LOWLAT = 0, 1, 2
+LOWLAT_MAX = 1024  # XSK_GPU_LOWLAT_MAX
+MULTI_MAX = 16  # XSK_GPU_MULTI_MAX
 
 # struct xsk_gpu_desc == struct xdp_desc (linux/if_xdp.h)
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
@@ -106,7 +110,16 @@ _SIGS = {
     "xsk_gpu_tx_complete": ([C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32], C.c_uint32),
     "xsk_gpu_classify_workspace_size": ([C.c_uint32], C.c_size_t),
     "xsk_gpu_classify_dev": ([_P, C.c_uint64, _P, C.c_uint32, C.c_int, _P, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu_multi_init": ([C.POINTER(_P), _P, C.c_uint32, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
+    "xsk_gpu_multi_process": ([_P, _P, C.c_uint32, _P, _P, _P], C.c_int),
+    "xsk_gpu_multi_set_options": ([_P, C.c_uint32], C.c_int),
+    "xsk_gpu_multi_fini": ([_P], None),
 }
+_TUNE_SIGS = {
+    "xsk_gpu__echo_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu__echo_wire_variant": ([C.c_int, _P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P], C.c_int),
+}
+_tune: Optional[C.CDLL] = None
 
 
 def lib() -> C.CDLL:
@@ -122,6 +135,22 @@ def lib() -> C.CDLL:
             fn.restype = res
         _lib = L
     return _lib
+
+
+def tune_lib() -> C.CDLL:
+    """libxsknet_amd_tune.so: the kernel variants of the tuning sweep (tests and tools/ only)."""
+    global _tune
+    if _tune is None:
+        lib()
+        if not os.path.exists(TUNE_LIB_PATH):
+            raise OSError(f"{TUNE_LIB_PATH} not built: run `make`")
+        L = C.CDLL(TUNE_LIB_PATH)
+        for name, (args, res) in _TUNE_SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _tune = L
+    return _tune
 
 
 def _check(fn: str, rc: int) -> None:
@@ -242,6 +271,49 @@ class EchoContext:
     def close(self) -> None:
         if self._ctx:
             lib().xsk_gpu_fini(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiContext:
+    """xsk_gpu_multi_*: one host UMEM, one context per entry of ``devices`` (repeats allowed), descriptor i
+    of a batch on context i mod G, counters summed."""
+
+    def __init__(self, umem: np.ndarray, devices, max_batch: int = 4096, mode: int = MODE_ZEROCOPY, opts: int = 0):
+        assert umem.dtype == np.uint8 and umem.flags.c_contiguous
+        self.umem = umem
+        self._ctx = C.c_void_p()
+        devs = (C.c_int * len(devices))(*devices)
+        _check("xsk_gpu_multi_init", lib().xsk_gpu_multi_init(C.byref(self._ctx), devs, len(devices), umem.ctypes.data,
+                                                              umem.nbytes, max_batch, mode))
+        if opts:
+            _check("xsk_gpu_multi_set_options", lib().xsk_gpu_multi_set_options(self._ctx, opts))
+
+    def process(self, descs: np.ndarray, want_recs: bool = True):
+        n = len(descs)
+        descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+        verdicts = np.zeros(n, np.uint8)
+        recs = np.zeros(n, REC_DTYPE) if want_recs else None
+        stats = np.zeros(1, STATS_DTYPE)
+        _check("xsk_gpu_multi_process", lib().xsk_gpu_multi_process(
+            self._ctx, descs.ctypes.data, n, verdicts.ctypes.data, recs.ctypes.data if recs is not None else None,
+            stats.ctypes.data))
+        return verdicts, recs, stats[0]
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().xsk_gpu_multi_fini(self._ctx)
             self._ctx = C.c_void_p()
 
     def __enter__(self):

@@ -10,9 +10,9 @@
 //   50-54 the shipped row-streaming kernel at other U (loads in flight) / occupancy settings
 #include <errno.h>
 
-#include "xsk_echo_device.h"
+#include "../xsk_echo_device.h"
+#include "../xsk_hip_util.h"
 #include "xsk_echo_variants.h"
-#include "xsk_hip_util.h"
 
 using namespace xskgpu;
 
@@ -423,3 +423,8 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
 }
 
 }  // extern "C"
+
+// The tuning library's own copy of the error hook (the product library's is hidden).
+extern "C" __attribute__((visibility("hidden"))) int xsk_gpu__hip_fail(hipError_t e) {
+    return e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
+}

@@ -1,7 +1,9 @@
-// xsk_wire.hip — wire-format widening of the gfx950 echo transform (build-added).
+// xsk_wire_v1.hip — TUNING LIBRARY ONLY (libxsknet_amd_tune.so): the first wire-format kernel,
+// superseded by the round kernel's WIRE mode (echo_kernel6<.., WIRE = true>, launched by
+// xsk_gpu_echo_dev_opts in xsk_echo.hip), kept for same-session comparisons (tools/wireab.py).
 //
-// xsk_gpu_echo_dev_opts() with nonzero XSK_GPU_OPT_* runs this kernel instead of the reference-exact
-// round kernel: the headers are parsed (802.1Q/802.1ad tags, IHL, tot_len, fragments) instead of read
+// Wire-format widening (build-added): with nonzero XSK_GPU_OPT_* the kernel works
+// instead of the reference-exact round kernel: the headers are parsed (802.1Q/802.1ad tags, IHL, tot_len, fragments) instead of read
 // at the fixed offsets of process_packet() (src/lib/xsk_receive.c:120-121), checksums can gate the
 // reply, and the reply rewrite of xsk_receive.c:148-157 lands at the parsed offsets.  The spec is the
 // comment block above XSK_GPU_OPT_STRICT_IPV4 in include/xsk_gpu.h; oracle_echo_batch_opts() restates it
@@ -17,8 +19,8 @@
 // inside the first 64 bytes leave as whole 64-B sectors; every other reply is patched byte-exact.
 #include <errno.h>
 
-#include "xsk_echo_device.h"
-#include "xsk_hip_util.h"
+#include "../xsk_echo_device.h"
+#include "../xsk_hip_util.h"
 
 using namespace xskgpu;
 
@@ -303,29 +305,22 @@ __global__ __launch_bounds__(NW * 64) void echo_wire_kernel(EchoArgs a, uint32_t
 
 }  // namespace
 
-// Implementation of the wire mode: 0 = the round kernel with WIRE (echo_kernel6<.., true>: one read of
-// every byte, the parse in the header phase; shipped), 1 = echo_wire_kernel (window first, then the
-// stream; kept for comparison).  Tuning switch only (xsk_gpu__set_wire_impl).
-static int g_wire_impl = 0;
-
 extern "C" {
 
-uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip
+uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip (product library)
 
-int xsk_gpu__set_wire_impl(int impl) {
-    if (impl < 0 || impl > 2) return -EINVAL;
-    g_wire_impl = impl;
-    return 0;
-}
-
-// Internal: wire-mode launch (xsk_gpu_echo_dev_opts in xsk_echo.hip validates the arguments).
-int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
-                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, void* d_partials,
-                           struct xsk_gpu_stats* d_stats, int fold, uint32_t* grid_out, void* stream) {
+// Wire-mode kernels for comparison: impl 1 = echo_wire_kernel (window first, then the stream), 2 = the
+// round kernel's WIRE mode with dot2 sums in the per-step streams.  Counters by device atomics into
+// d_stats (device memory) or none.  Validation is the caller's (tools only).
+int xsk_gpu__echo_wire_variant(int impl, void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs,
+                               uint32_t n, uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
+                               struct xsk_gpu_stats* d_stats, void* stream) {
+    if (n == 0) return 0;
+    if (!opts || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
     int device = 0;
     HIP_TRY(hipGetDevice(&device));
     const uint32_t ncu = xsk_gpu__num_cu(device);
-    if (!ncu) return xsk_gpu__hip_fail(hipErrorInvalidDevice);
+    if (!ncu) return -ENODEV;
     uint32_t grid = 0, tiles_per_wg = 0;
     echo6_geometry(n, ncu, &grid, &tiles_per_wg);
     EchoArgs args;
@@ -335,23 +330,18 @@ int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gp
     args.n = n;
     args.verdicts = d_verdicts;
     args.recs = d_recs;
-    args.partials = (unsigned long long*)d_partials;
+    args.partials = nullptr;
     args.opts = opts;
-    if (d_stats && (grid == 1 || !fold)) {  // the workgroups add their counters themselves (no fold launch)
-        args.partials = nullptr;
-        args.stats_direct = (unsigned long long*)&d_stats->rx_packets;
-    }
-    if (g_wire_impl == 0)
-        echo_kernel6<kShip6U, 1, 2, 2, false, false, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(
-            args, tiles_per_wg);
-    else if (g_wire_impl == 2)  // + dot2 sums in the per-step streams
+    args.stats_direct = d_stats ? (unsigned long long*)&d_stats->rx_packets : nullptr;
+    if (impl == 2)
         echo_kernel6<kShip6U, 1, 2, 2, false, false, true, false, false, false, true>
             <<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, tiles_per_wg);
-    else
+    else if (impl == 1)
         echo_wire_kernel<kWireU, kWaves6, true><<<dim3(grid), dim3(kThreads6), 0, (hipStream_t)stream>>>(args, opts,
                                                                                                        tiles_per_wg);
+    else
+        return -EINVAL;
     HIP_TRY(hipGetLastError());
-    *grid_out = grid;
     return 0;
 }
 

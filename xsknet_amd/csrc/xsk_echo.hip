@@ -1,10 +1,13 @@
-// xsk_echo.hip — the product entry point of the gfx950 ICMP-echo transform: xsk_gpu_echo_dev() (one
-// launch of the round kernel echo_kernel6 + the counter fold), the workspace query, the kernel timer the bench reads,
-// and the error plumbing of the C ABI (include/xsk_gpu.h).  Device code: xsk_echo_device.h.
+// xsk_echo.hip — the product entry points of the gfx950 ICMP-echo transform: xsk_gpu_echo_dev() and
+// xsk_gpu_echo_dev_opts() (one launch of the round kernel echo_kernel6, reference or wire mode), the
+// workspace query, the kernel timer the bench reads, and the error plumbing of the C ABI
+// (include/xsk_gpu.h).  Device code: xsk_echo_device.h.  Tuning variants live in the separate
+// libxsknet_amd_tune.so (tune/), never in this library.
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 
 #include "xsk_echo_device.h"
@@ -16,6 +19,7 @@ namespace {
 
 // Fold the per-workgroup partials into the caller's stats_record-compatible counters: 1024 threads,
 // thread t sums counter t % 4 over rows t/4, t/4 + 256, ... with 4 independent chains, then a tree.
+// Only for counters in mapped host memory (device atomics are not an option there).
 __global__ __launch_bounds__(1024) void fold_counters_kernel(const unsigned long long* partials, uint32_t nwg,
                                                             xsk_gpu_stats* st) {
     __shared__ unsigned long long s[1024];
@@ -41,31 +45,54 @@ __global__ __launch_bounds__(1024) void fold_counters_kernel(const unsigned long
 
 thread_local const char* g_last_error = "ok";
 
-// Counter delivery of xsk_gpu_echo_dev(_opts): 1 = every workgroup adds its four counters to d_stats with
-// device-scope atomics (shipped: 1.5-2.5 % less time per call than the fold launch, profiles/r01/stats_delivery.log);
-// 0 = per-workgroup partials + the fold launch.  Tuning switch: xsk_gpu__set_stats_atomic.
-int g_stats_atomic = 1;
-
 // ---- kernel timing (bench instrumentation) -------------------------------------------------------
-constexpr int kTimerCap = 8192;
+// Events are created per device, lazily, on the device of the launch they bracket; a slot is claimed
+// only once its start event has been recorded.
+constexpr int kTimerCap = 4096;
+constexpr int kMaxDev = 64;
+struct TimerPool {
+    hipEvent_t ev[kTimerCap][2];
+};
 struct Timer {
     bool on = false;
-    int count = 0;  // recorded pairs since enable
-    hipEvent_t ev[kTimerCap][2];
-    bool created = false;
-    int dev[kTimerCap];
+    int count = 0;              // claimed slots since enable
+    int dev[kTimerCap];         // device of slot i; -1 when its end event failed to record
+    TimerPool* pool[kMaxDev] = {};
 };
 Timer g_timer;
 std::mutex g_timer_mu;
 
-// Timer slot for the next transform launch (-1 when timing is off or full).
-int timer_slot(int device) {
+int timer_begin(int device, hipStream_t s) {
     std::lock_guard<std::mutex> lk(g_timer_mu);
-    if (!g_timer.on || g_timer.count >= kTimerCap) return -1;
-    const int slot = g_timer.count++;
+    if (!g_timer.on || g_timer.count >= kTimerCap || device < 0 || device >= kMaxDev) return -1;
+    TimerPool*& p = g_timer.pool[device];
+    if (!p) {  // the current device is `device`: create its events here
+        TimerPool* np = new (std::nothrow) TimerPool;
+        if (!np) return -1;
+        for (int i = 0; i < kTimerCap; ++i) {
+            if (hipEventCreate(&np->ev[i][0]) != hipSuccess || hipEventCreate(&np->ev[i][1]) != hipSuccess) {
+                delete np;  // (events leak on this rare path; timing is bench instrumentation)
+                return -1;
+            }
+        }
+        p = np;
+    }
+    const int slot = g_timer.count;
+    if (hipEventRecord(p->ev[slot][0], s) != hipSuccess) return -1;
     g_timer.dev[slot] = device;
+    g_timer.count++;
     return slot;
 }
+
+void timer_end(int slot, hipStream_t s) {
+    if (slot < 0) return;
+    std::lock_guard<std::mutex> lk(g_timer_mu);
+    const int d = g_timer.dev[slot];
+    if (d < 0 || hipEventRecord(g_timer.pool[d]->ev[slot][1], s) != hipSuccess) g_timer.dev[slot] = -1;
+}
+
+// Compute units per device, looked up once (the round kernel launches one workgroup per CU).
+std::atomic<int> g_num_cu[kMaxDev];
 
 }  // namespace
 
@@ -84,47 +111,47 @@ const char* xsk_gpu_last_error(void) { return g_last_error; }
 
 size_t xsk_gpu_workspace_size(int device, uint32_t n) {
     if (device < 0) return 0;
-    // room for the partial rows of either launch geometry (round kernel: <= one workgroup per CU)
+    // room for the partial rows of the round kernel's grid (<= one workgroup per CU)
     const uint32_t ntiles = (n + kTile - 1) / kTile;
-    uint32_t g = echo_grid(n);
-    const uint32_t g6 = ntiles < kMaxCuBound ? ntiles : kMaxCuBound;
-    if (g6 > g) g = g6;
+    uint32_t g = ntiles < kMaxCuBound ? ntiles : kMaxCuBound;
+    if (g < 1) g = 1;
     return (size_t)g * 4 * sizeof(unsigned long long);
 }
 
-// Compute units of `device` (cached): the round kernel launches one workgroup per CU.
+// Compute units of `device` (cached, race-free: concurrent first lookups store the same value).
 uint32_t xsk_gpu__num_cu(int device) {
-    static int cache[64];
-    if (device < 0 || device >= 64) return 0;
-    if (cache[device] <= 0) {
-        int v = 0;
+    if (device < 0 || device >= kMaxDev) return 0;
+    int v = g_num_cu[device].load(std::memory_order_relaxed);
+    if (v <= 0) {
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) return 0;
-        cache[device] = v > (int)kMaxCuBound ? (int)kMaxCuBound : v;
+        if (v > (int)kMaxCuBound) v = (int)kMaxCuBound;
+        g_num_cu[device].store(v, std::memory_order_relaxed);
     }
-    return (uint32_t)cache[device];
+    return (uint32_t)v;
 }
 
-
-// fold = 1: per-workgroup partials in the workspace + the one-workgroup fold launch (the stats may live in
-// mapped host memory, where device-scope atomics are not an option); 0: every workgroup adds its counters to
-// d_stats (device memory) with device-scope atomics, no second launch.
-static int echo_dev_impl(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
-                         uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
-                         void* d_workspace, void* stream, int fold) {
+// One transform launch (reference mode for opts == 0, wire mode otherwise).  Counters: device memory
+// (hoststats == 0) -> every workgroup adds its four counters with device-scope atomics, one launch;
+// mapped host memory (hoststats == 1, the zerocopy host context) -> a one-workgroup launch adds them
+// itself, a larger grid writes per-workgroup partials that a one-workgroup fold launch adds.
+static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t opts,
+                       uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
+                       void* d_workspace, void* stream, int hoststats) {
+    if (opts & ~XSK_GPU_OPT_ALL) return -EINVAL;
     if (n == 0) return 0;
     if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
     if (!d_umem || !d_descs || ((uintptr_t)d_umem & 15u) || (umem_size & 15u) || ((uintptr_t)d_descs & 15u) ||
         ((uintptr_t)d_recs & 15u))
         return -EINVAL;
     if (d_stats && !d_workspace) return -EINVAL;
-    if (umem_size >> 48) return -EINVAL;  // FrameMeta6 carries 48-bit UMEM offsets
+    if (umem_size >> 48) return -EINVAL;  // FrameMeta6 carries 48-bit UMEM offsets (both modes)
     int device = 0;
     HIP_TRY(hipGetDevice(&device));
     const uint32_t ncu = xsk_gpu__num_cu(device);
     if (!ncu) return xsk_gpu__hip_fail(hipErrorInvalidDevice);
     uint32_t grid = 0, tiles_per_wg = 0;
     echo6_geometry(n, ncu, &grid, &tiles_per_wg);
-    hipStream_t s = (hipStream_t)stream;
+    const hipStream_t s = (hipStream_t)stream;
     EchoArgs args;
     args.umem = (uint8_t*)d_umem;
     args.umem_size = umem_size;
@@ -132,20 +159,31 @@ static int echo_dev_impl(void* d_umem, uint64_t umem_size, const struct xsk_gpu_
     args.n = n;
     args.verdicts = d_verdicts;
     args.recs = d_recs;
-    args.partials = d_stats ? (unsigned long long*)d_workspace : nullptr;
-    if (d_stats && (grid == 1 || !fold)) {  // the workgroups add their counters themselves
-        args.partials = nullptr;
-        args.stats_direct = (unsigned long long*)&d_stats->rx_packets;
+    args.partials = nullptr;
+    args.opts = opts;
+    bool fold = false;
+    if (d_stats) {
+        if (!hoststats) {
+            args.stats_direct = (unsigned long long*)&d_stats->rx_packets;
+        } else if (grid == 1) {
+            args.stats_direct = (unsigned long long*)&d_stats->rx_packets;
+            args.stats_plain = 1;
+        } else {
+            args.partials = (unsigned long long*)d_workspace;
+            fold = true;
+        }
     }
-
-    const int slot = timer_slot(device);
-    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], s));
-    echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2,
-                 kShip6Skm>
-        <<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    HIP_TRY(hipGetLastError());
-    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], s));
-    if (d_stats && grid > 1 && fold) {
+    const int slot = timer_begin(device, s);
+    if (opts == 0)
+        echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2,
+                     kShip6Skm><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+    else  // wire mode: 128-B windows, one tile per wave per round
+        echo_kernel6<kShip6U, 1, kShip6Sync, kShip6Stream, false, false, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(
+            args, tiles_per_wg);
+    const hipError_t le = hipGetLastError();
+    timer_end(slot, s);
+    if (le != hipSuccess) return xsk_gpu__hip_fail(le);
+    if (fold) {
         hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, s, (const unsigned long long*)d_workspace, grid,
                            d_stats);
         HIP_TRY(hipGetLastError());
@@ -156,72 +194,24 @@ static int echo_dev_impl(void* d_umem, uint64_t umem_size, const struct xsk_gpu_
 int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                      void* d_workspace, void* stream) {
-    return echo_dev_impl(d_umem, umem_size, d_descs, n, d_verdicts, d_recs, d_stats, d_workspace, stream,
-                         !g_stats_atomic);
-}
-
-int xsk_gpu__echo_wire_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
-                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, void* d_partials,
-                           struct xsk_gpu_stats* d_stats, int fold, uint32_t* grid_out, void* stream);  // xsk_wire.hip
-
-static int echo_dev_opts_impl(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
-                              uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
-                              struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream, int fold) {
-    if (opts & ~XSK_GPU_OPT_ALL) return -EINVAL;
-    if (opts == 0)
-        return echo_dev_impl(d_umem, umem_size, d_descs, n, d_verdicts, d_recs, d_stats, d_workspace, stream, fold);
-    if (n == 0) return 0;
-    if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
-    if (!d_umem || !d_descs || ((uintptr_t)d_umem & 15u) || (umem_size & 15u) || ((uintptr_t)d_descs & 15u) ||
-        ((uintptr_t)d_recs & 15u))
-        return -EINVAL;
-    if (d_stats && !d_workspace) return -EINVAL;
-    int device = 0;
-    HIP_TRY(hipGetDevice(&device));
-    uint32_t grid = 0;
-    const int slot = timer_slot(device);
-    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][0], (hipStream_t)stream));
-    const int rc = xsk_gpu__echo_wire_dev(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs,
-                                          d_stats ? d_workspace : nullptr, d_stats, fold, &grid, stream);
-    if (rc) return rc;
-    if (slot >= 0) HIP_TRY(hipEventRecord(g_timer.ev[slot][1], (hipStream_t)stream));
-    if (d_stats && grid > 1 && fold) {  // otherwise the workgroups added their counters themselves
-        hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
-                           (const unsigned long long*)d_workspace, grid, d_stats);
-        HIP_TRY(hipGetLastError());
-    }
-    return 0;
+    return echo_launch(d_umem, umem_size, d_descs, n, 0, d_verdicts, d_recs, d_stats, d_workspace, stream, 0);
 }
 
 int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
                           struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream) {
-    return echo_dev_opts_impl(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream,
-                              !g_stats_atomic);
+    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 0);
 }
 
-// Internal (xsk_gpu_host.c, zerocopy mode): d_stats is mapped pinned host memory -> always the fold.
+// Internal (xsk_gpu_host.c, zerocopy mode): d_stats is mapped pinned host memory -> no device atomics.
 int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                                      uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
                                      struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream) {
-    return echo_dev_opts_impl(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 1);
-}
-
-int xsk_gpu__set_stats_atomic(int on) {
-    if (on < 0 || on > 1) return -EINVAL;
-    g_stats_atomic = on;
-    return 0;
+    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 1);
 }
 
 int xsk_gpu_timing_enable(int enable) {
     std::lock_guard<std::mutex> lk(g_timer_mu);
-    if (enable && !g_timer.created) {
-        for (int i = 0; i < kTimerCap; ++i) {
-            HIP_TRY(hipEventCreate(&g_timer.ev[i][0]));
-            HIP_TRY(hipEventCreate(&g_timer.ev[i][1]));
-        }
-        g_timer.created = true;
-    }
     g_timer.on = enable != 0;
     g_timer.count = 0;
     return 0;
@@ -230,14 +220,18 @@ int xsk_gpu_timing_enable(int enable) {
 int xsk_gpu_timing_read(double* total_ms, uint64_t* launches) {
     std::lock_guard<std::mutex> lk(g_timer_mu);
     double tot = 0.0;
+    uint64_t cnt = 0;
     for (int i = 0; i < g_timer.count; ++i) {
-        HIP_TRY(hipEventSynchronize(g_timer.ev[i][1]));
+        const int d = g_timer.dev[i];
+        if (d < 0) continue;
+        HIP_TRY(hipEventSynchronize(g_timer.pool[d]->ev[i][1]));
         float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, g_timer.ev[i][0], g_timer.ev[i][1]));
+        HIP_TRY(hipEventElapsedTime(&ms, g_timer.pool[d]->ev[i][0], g_timer.pool[d]->ev[i][1]));
         tot += ms;
+        cnt++;
     }
     if (total_ms) *total_ms = tot;
-    if (launches) *launches = (uint64_t)g_timer.count;
+    if (launches) *launches = cnt;
     g_timer.count = 0;
     return 0;
 }

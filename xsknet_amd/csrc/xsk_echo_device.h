@@ -1,5 +1,5 @@
 // xsk_echo_device.h — device code of the gfx950 (MI355X / CDNA4) ICMP-echo transform, shared by the
-// shipped entry point (xsk_echo.hip) and the tuning variants (xsk_tune.hip).
+// shipped entry point (xsk_echo.hip) and the tuning library (tune/xsk_tune.hip, not linked into the product).
 //
 // Replaces, for a whole batch of AF_XDP descriptors at once, the per-frame call
 //   process_packet()   /root/reference/src/lib/xsk_receive.c:113-190   (gates, field swap, type 8->0,
@@ -31,8 +31,10 @@ struct EchoArgs {
     xsk_gpu_rec* recs;
     unsigned long long* partials;  // [gridDim.x][4]: rx_packets, rx_bytes, tx_packets, tx_bytes
     uint32_t opts = 0;             // XSK_GPU_OPT_* (wire-mode kernels only)
-    // one-workgroup launches: add the counters straight into the caller's stats (no fold launch)
+    // every workgroup adds its counters straight into the caller's stats (no fold launch):
+    // device-scope atomics, or -- stats_plain, a one-workgroup launch on mapped host memory -- plain adds
     unsigned long long* stats_direct = nullptr;  // &stats->rx_packets (4 consecutive u64)
+    uint32_t stats_plain = 0;
 };
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -80,7 +82,7 @@ __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, un
         unsigned long long s = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) s += s_cnt[w][threadIdx.x];
-        if (a.stats_direct && gridDim.x == 1) a.stats_direct[threadIdx.x] += s;
+        if (a.stats_direct && a.stats_plain) a.stats_direct[threadIdx.x] += s;  // sole writer (host memory)
         else if (a.stats_direct)  // every workgroup adds its own: non-returning device-scope atomics
             __hip_atomic_fetch_add(a.stats_direct + threadIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else a.partials[blockIdx.x * 4 + threadIdx.x] = s;
@@ -841,18 +843,33 @@ constexpr uint32_t kHeavyLen = 1024;
 // the header phase's IPv4 sum with fixed masks when every frame has its whole header.
 // SKM: ranked streams mask only slots where a frame ends and rank small-row tiles by counting; uniform
 // short / ping-size tiles compute their ICMP byte masks once per tile.
+// LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB in reference mode).
+template <int TPW, bool WIRE, int STREAM>
+struct Echo6Smem {
+    static constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;
+    __attribute__((aligned(16))) uint8_t hdr[kWaves6][TPW][kTile * kRowW];  // 128 KiB: header windows
+    __attribute__((aligned(16))) FrameMeta6 meta[kWaves6][kTile];          // 16 KiB
+    uint32_t sum[kWaves6][2][kTile];                                        // 8 KiB
+    uint32_t sort[STREAM >= 1 ? kWaves6 : 1][80];                          // 5 KiB (STREAM 1, 2)
+    unsigned long long cnt[kWaves6][4];
+    uint32_t arrive;
+};
+
+// The round kernel's work over the tiles [t_begin, t_end) of one workgroup (every wave of the
+// workgroup calls it with the same range): rounds of kWaves6 * TPW tiles, read phase, write phase, and
+// the counters (store_partials).  echo_kernel6 runs it once per workgroup on its static share; the
+// low-latency persistent kernel (xsk_lowlat.hip) once per doorbell.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false>
-__global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
+__device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
+                                           Echo6Smem<TPW, WIRE, STREAM>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
     const uint64_t wgt_start = WGT ? wall_clock64() : 0ull;
-    __shared__ __attribute__((aligned(16))) uint8_t s_hdr[kWaves6][TPW][kTile * kRowW];  // 128 KiB
-    __shared__ __attribute__((aligned(16))) FrameMeta6 s_meta[kWaves6][kTile];          // 16 KiB
-    __shared__ uint32_t s_sum[kWaves6][2][kTile];                                        // 8 KiB
-    __shared__ uint32_t s_sort[STREAM >= 1 ? kWaves6 : 1][80];                          // 5 KiB (STREAM 1, 2)
-    __shared__ unsigned long long s_cnt[kWaves6][4];
-    __shared__ uint32_t s_arrive;
+    auto& s_hdr = sm.hdr;
+    auto& s_sort = sm.sort;
+    auto& s_cnt = sm.cnt;
+    uint32_t& s_arrive = sm.arrive;
     if (SYNC == 2) {
         if (threadIdx.x == 0) s_arrive = 0u;
         __syncthreads();
@@ -860,12 +877,9 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
     uint32_t rounds_done = 0;
 
     const uint32_t wave = uniform(threadIdx.x >> 6);
-    FrameMeta6* meta = s_meta[wave];
-    uint32_t* sums_ic = s_sum[wave][0];
-    uint32_t* sums_ip = s_sum[wave][1];
-    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
-    const uint32_t t_begin = blockIdx.x * tiles_per_wg;
-    const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+    FrameMeta6* meta = sm.meta[wave];
+    uint32_t* sums_ic = sm.sum[wave][0];
+    uint32_t* sums_ip = sm.sum[wave][1];
     constexpr uint32_t kRound = (uint32_t)kWaves6 * TPW;
     Counters cnt;
     uint32_t lane = threadIdx.x & 63u;
@@ -959,7 +973,6 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
                     // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
                     // nothing lies past byte 128, so the streamed part of every sum is zero
                     const uint32_t kk = lane & 7u, ro = 16u * kk;
-                    const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
                     u32x4 x[8];
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
@@ -1172,6 +1185,17 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         a.partials[8192 + 2 * blockIdx.x] = wgt_start;
         a.partials[8192 + 2 * blockIdx.x + 1] = wall_clock64();
     }
+}
+
+// One 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg tiles (echo6_geometry).
+template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false>
+__global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
+    __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t_begin = blockIdx.x * tiles_per_wg;
+    const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+    echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM>(a, t_begin, t_end, tiles_per_wg, sm);
 }
 
 

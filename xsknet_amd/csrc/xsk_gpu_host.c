@@ -11,6 +11,8 @@
  *             over PCIe in place, reads the descriptors from a mapped pinned staging buffer and writes
  *             verdicts and counters straight into mapped pinned host memory: a batch is one kernel
  *             launch (two when it spans more than one workgroup) and one synchronisation, no copies.
+ *   LOWLAT:   ZEROCOPY, but batches of <= XSK_GPU_LOWLAT_MAX frames go to a resident polling kernel
+ *             through a doorbell in mapped host memory (xsk_lowlat.hip): no launch, no synchronisation.
  *   STAGED:   frames are copied host->device into a device mirror of the UMEM (one strided 2-D copy
  *             when the chunk has a uniform frame stride, else the chunk's byte span), transformed in
  *             HBM, and only the 38 rewritten header bytes of TX_REPLY frames are copied back and
@@ -26,14 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../include/xsk_gpu.h"
-
-int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs, const uint8_t* d_verdicts,
-                              uint32_t n, uint8_t* d_pack, uint32_t wire, void* stream);
-/* xsk_gpu_echo_dev_opts for counters in mapped host memory (always the fold launch, no device atomics) */
-int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
-                                     uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
-                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream);
+#include "xsk_gpu_internal.h"
 
 #define NSTREAMS 2
 #define CHUNK_FRAMES 32768u /* staged pipeline granule: ~49 MB of 1500-B frames per copy-in */
@@ -64,8 +59,12 @@ struct xsk_gpu_ctx {
     struct xsk_gpu_stats* m_stats;
     hipStream_t stream[NSTREAMS];
     hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
-    int registered;
+    int registered;   /* this context registered the UMEM (and unregisters it at fini) */
+    xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
 };
+
+/* ZEROCOPY and LOWLAT read the UMEM in place through its mapped alias */
+static int zerocopy(const xsk_gpu_ctx* c) { return c->mode != XSK_GPU_MODE_STAGED; }
 
 static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO; }
 #define TRY(expr)                           \
@@ -80,6 +79,7 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    xsk_gpu__lowlat_free(c->ll);
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamSynchronize(c->stream[s]);
     if (c->mode == XSK_GPU_MODE_STAGED && c->d_umem) (void)hipFree(c->d_umem);
@@ -104,10 +104,12 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
     free(c);
 }
 
-int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
+static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode,
+                     int prereg) {
     int rc = 0;
     if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || max_batch == 0 ||
-        max_batch > XSK_GPU_MAX_BATCH || (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED))
+        max_batch > XSK_GPU_MAX_BATCH ||
+        (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED && mode != XSK_GPU_MODE_LOWLAT))
         return -EINVAL;
     *out = NULL;
     int ndev = 0;
@@ -122,9 +124,11 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
     c->max_chunks = mode == XSK_GPU_MODE_STAGED ? (max_batch + CHUNK_FRAMES - 1) / CHUNK_FRAMES : 1;
     TRY(hipSetDevice(device));
     for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamCreateWithFlags(&c->stream[s], hipStreamNonBlocking));
-    TRY(hipHostRegister(umem, umem_size, mode == XSK_GPU_MODE_ZEROCOPY ? hipHostRegisterMapped : hipHostRegisterDefault));
-    c->registered = 1;
-    if (mode == XSK_GPU_MODE_ZEROCOPY) {
+    if (!prereg) {
+        TRY(hipHostRegister(umem, umem_size, zerocopy(c) ? hipHostRegisterMapped : hipHostRegisterDefault));
+        c->registered = 1;
+    }
+    if (zerocopy(c)) {
         TRY(hipHostGetDevicePointer((void**)&c->d_umem, umem, 0));
     } else {
         TRY(hipMalloc((void**)&c->d_umem, umem_size));
@@ -136,7 +140,7 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
     TRY(hipMalloc((void**)&c->d_recs, (size_t)max_batch * sizeof(struct xsk_gpu_rec)));
     TRY(hipMalloc((void**)&c->d_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats)));
     {
-        const uint32_t per = max_batch < CHUNK_FRAMES || mode == XSK_GPU_MODE_ZEROCOPY ? max_batch : CHUNK_FRAMES;
+        const uint32_t per = max_batch < CHUNK_FRAMES || zerocopy(c) ? max_batch : CHUNK_FRAMES;
         const size_t ws = xsk_gpu_workspace_size(device, per);
         if (ws == 0) {
             rc = -EIO;
@@ -146,7 +150,7 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
     }
     TRY(hipHostMalloc((void**)&c->h_verd, max_batch, hipHostMallocMapped));
     TRY(hipHostMalloc((void**)&c->h_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats), hipHostMallocMapped));
-    if (mode == XSK_GPU_MODE_ZEROCOPY) {
+    if (zerocopy(c)) {
         TRY(hipHostMalloc((void**)&c->h_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc), hipHostMallocMapped));
         TRY(hipHostGetDevicePointer((void**)&c->m_descs, c->h_descs, 0));
         TRY(hipHostGetDevicePointer((void**)&c->m_verd, c->h_verd, 0));
@@ -158,12 +162,26 @@ int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, 
         goto out;
     }
     for (uint32_t i = 0; i < c->max_chunks; i++) TRY(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
+    if (mode == XSK_GPU_MODE_LOWLAT) {
+        rc = xsk_gpu__lowlat_start(&c->ll, c->d_umem, umem_size, 0);
+        if (rc) goto out;
+    }
     *out = c;
     return 0;
 out:
     xsk_gpu_fini(c);
     return rc;
 }
+
+int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
+    return init_impl(out, device, umem, umem_size, max_batch, mode, 0);
+}
+
+int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
+    return init_impl(out, device, umem, umem_size, max_batch, mode, 1);
+}
+
+uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* c) { return c ? c->max_batch : 0u; }
 
 /* Uniform stride S (>= 64, multiple of 16) when addr[i] = addr[0] + i*S for the whole chunk. */
 static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
@@ -178,6 +196,11 @@ static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
 
 int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     if (!c || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
+    if (c->ll) {
+        (void)hipSetDevice(c->device);
+        const int rc = xsk_gpu__lowlat_set_opts(c->ll, opts);
+        if (rc) return rc;
+    }
     c->opts = opts;
     return 0;
 }
@@ -217,7 +240,7 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
                          int want_recs, int s) {
     int rc = 0;
     const hipStream_t st = c->stream[s];
-    if (c->mode == XSK_GPU_MODE_ZEROCOPY) { /* descriptors in, verdicts and counters out: mapped host memory */
+    if (zerocopy(c)) { /* descriptors in, verdicts and counters out: mapped host memory */
         memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
         memset(&c->h_stats[ci], 0, sizeof c->h_stats[ci]);
         rc = xsk_gpu__echo_dev_opts_hoststats(c->d_umem, c->umem_size, c->m_descs + i0, n, c->opts, c->m_verd + i0,
@@ -257,6 +280,22 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
     if (n == 0) return 0;
     if (n > c->max_batch) return -EINVAL;
     TRY(hipSetDevice(c->device));
+    if (c->ll && n <= XSK_GPU_LOWLAT_MAX) { /* the doorbell: no launch, no synchronisation */
+        memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
+        rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL);
+        if (rc) return rc;
+        const struct xsk_gpu_stats* hs = xsk_gpu__lowlat_stats(c->ll);
+        if (verdicts) memcpy(verdicts, xsk_gpu__lowlat_verdicts(c->ll), n);
+        if (recs) memcpy(recs, xsk_gpu__lowlat_recs(c->ll), (size_t)n * sizeof *recs);
+        if (stats) {
+            stats->rx_packets += hs->rx_packets;
+            stats->rx_bytes += hs->rx_bytes;
+            stats->tx_packets += hs->tx_packets;
+            stats->tx_bytes += hs->tx_bytes;
+        }
+        return 0;
+    }
+    if (c->ll) xsk_gpu__lowlat_stop(c->ll); /* a large batch: the launch path (its streams never wait on it) */
     const uint32_t chunk = c->mode == XSK_GPU_MODE_STAGED ? CHUNK_FRAMES : n;
     const uint32_t nchunks = (n + chunk - 1) / chunk;
     for (uint32_t ci = 0; ci < nchunks; ci++) {

@@ -1,0 +1,69 @@
+/*
+ * xsk_gpu_internal.h — symbols shared between the translation units of libxsknet_amd.so that are not
+ * part of the public C ABI (include/xsk_gpu.h).  C11 and C++ (HIP) both include it.
+ */
+#ifndef XSK_GPU_INTERNAL_H
+#define XSK_GPU_INTERNAL_H
+
+#include "../../include/xsk_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XSK_GPU__HIDDEN __attribute__((visibility("hidden")))
+
+/* xsk_aux.hip: staged mode's gather of the rewritten header bytes of TX_REPLY frames */
+XSK_GPU__HIDDEN int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_descs,
+                                              const uint8_t* d_verdicts, uint32_t n, uint8_t* d_pack, uint32_t wire,
+                                              void* stream);
+
+/* xsk_echo.hip: xsk_gpu_echo_dev_opts for counters in mapped host memory (no device atomics) */
+XSK_GPU__HIDDEN int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size,
+                                                     const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t opts,
+                                                     uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
+                                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream);
+
+/* xsk_gpu_host.c: xsk_gpu_init over a UMEM the caller has already registered with the HIP runtime
+ * (portable + mapped, e.g. the one registration of a multi-GPU object): the context neither registers
+ * nor unregisters it. */
+XSK_GPU__HIDDEN int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size,
+                                         uint32_t max_batch, int mode);
+XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
+
+/* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context.  Shared memory
+ * layout (mapped, fine-grained pinned host memory): host-written and device-written words live on
+ * separate 128-byte lines. */
+struct xsk_gpu__bell {
+    /* host -> device */
+    volatile uint32_t seq;   /* bumped by one per posted batch                               */
+    volatile uint32_t n;     /* frames of the posted batch (<= XSK_GPU_LOWLAT_MAX)             */
+    volatile uint32_t recs;  /* nonzero: write records                                        */
+    volatile uint32_t stop;  /* nonzero: the persistent kernel exits at its next poll          */
+    uint32_t pad0[28];
+    /* device -> host */
+    volatile uint32_t done;  /* seq of the last completed batch                               */
+    volatile uint32_t alive; /* 1 while the persistent kernel runs                            */
+    uint32_t pad1[30];
+};
+
+typedef struct xsk_gpu__lowlat xsk_gpu__lowlat;
+/* Create the channel on the current device for the (mapped) UMEM alias d_umem: its doorbell, mapped
+ * buffers and stream.  The persistent kernel starts with the first batch. */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_size, uint32_t opts);
+XSK_GPU__HIDDEN void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll);
+/* Post the batch already written into the mapped descriptor buffer and wait for its completion. */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs);
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts);
+XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
+/* Mapped host buffers the kernel reads / writes: descriptors, verdicts, records, counters. */
+XSK_GPU__HIDDEN struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll);
+XSK_GPU__HIDDEN uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll);
+XSK_GPU__HIDDEN struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll);
+XSK_GPU__HIDDEN struct xsk_gpu_stats* xsk_gpu__lowlat_stats(xsk_gpu__lowlat* ll);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XSK_GPU_INTERNAL_H */

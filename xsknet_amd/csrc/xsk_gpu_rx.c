@@ -7,7 +7,7 @@
 #include <errno.h>
 #include <string.h>
 
-#include "../../include/xsk_gpu.h"
+#include "xsk_gpu_internal.h"
 #include "xsk_ring.h"
 
 static inline void pool_push(struct xsk_gpu_frame_pool* p, uint64_t a) {
@@ -22,13 +22,16 @@ int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ri
     struct xsk_gpu_rx_result r = {0, 0, 0, 0};
     if (!ctx || !rx || !fill || !tx || !pool || !pool->addr || max_batch == 0) return -EINVAL;
     if (max_batch > XSK_GPU_RX_MAX_STEP) max_batch = XSK_GPU_RX_MAX_STEP;
-
-    uint32_t idx_rx = 0;
-    const uint32_t rcvd = xr_cons_peek(rx, max_batch, &idx_rx); /* :196 */
-    if (!rcvd) {
+    if (!xr_cons_avail(rx, 1)) { /* nothing received: the context is not even looked at */
         if (res) *res = r;
         return 0;
     }
+    /* never peek more than the context takes: xsk_gpu_process would refuse the batch after the fill
+       ring had been restocked, and a caller retrying the step would spin on the same error */
+    if (max_batch > xsk_gpu__ctx_max_batch(ctx)) max_batch = xsk_gpu__ctx_max_batch(ctx);
+
+    uint32_t idx_rx = 0;
+    const uint32_t rcvd = xr_cons_peek(rx, max_batch, &idx_rx); /* :196 */
     /* :201-217 — stock the fill ring from the free-frame stack */
     uint32_t stock = xr_prod_free(fill, pool->n_free);
     if (stock > pool->n_free) stock = pool->n_free;

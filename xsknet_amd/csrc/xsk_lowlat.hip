@@ -1,0 +1,280 @@
+// xsk_lowlat.hip — the low-latency RX-loop channel of an XSK_GPU_MODE_LOWLAT host context.
+//
+// The reference hands its transform RX_BATCH_SIZE = 64 descriptors per poll() (src/lib/xsk_receive.c:196,
+// :251-257; src/lib/xsk_utils.h:8).  At that size a kernel launch plus a stream synchronisation costs
+// far more than the work, so this channel keeps ONE workgroup of the round kernel
+// resident: it polls a doorbell in fine-grained pinned host memory, runs the round kernel's body
+// (echo6_body, xsk_echo_device.h — the same code the launched kernel runs, bit for bit) over the posted
+// descriptors, writes verdicts, records and counters into mapped host memory, and publishes completion.
+// A batch is "write descriptors, bump the doorbell, spin on the completion word": no launch, no sync.
+//
+// Memory ordering (AMDGPU memory model, system scope): the host stores descriptors, then the doorbell
+// sequence number (x86 TSO keeps the order).  Thread 0 of the kernel reads the doorbell with a system-
+// scope acquire; after the workgroup barrier every wave issues a system-scope acquire fence, which
+// invalidates the CU's L1 and the L2 lines of host memory, so recycled UMEM frames are never read stale.
+// After the body every wave issues a system-scope release fence (its stores to the UMEM, verdicts and
+// counters are performed and the L2 written back), the workgroup meets, and thread 0 stores the batch's
+// sequence number to `done` with a system-scope release.
+//
+// Exit conditions every wave reaches: the host's stop word, or no batch for kIdleTicks (50 ms of the
+// 100-MHz wall clock) — so a process that dies without xsk_gpu_fini() never leaves the grid running.
+// The host relaunches the kernel lazily when it finds it gone (alive == 0 before posting, or the
+// kernel's stream idle while a batch waits).  The exit path is Dekker-safe: the kernel clears `alive`,
+// then looks at the doorbell once more and resumes if a batch slipped in.
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "xsk_echo_device.h"
+#include "xsk_gpu_internal.h"
+#include "xsk_hip_util.h"
+
+using namespace xskgpu;
+
+namespace {
+
+constexpr uint64_t kIdleTicks = 5000000ull;  // 50 ms at 100 MHz (s_memrealtime)
+constexpr int kLLTPW = 1;                    // 16 tiles = 1024 frames per doorbell, one round
+constexpr int kLLSync = 0;                   // one round: write as soon as the wave has read
+
+struct LowlatArgs {
+    xsk_gpu__bell* bell;  // device alias of the mapped doorbell
+    uint8_t* umem;
+    uint64_t umem_size;
+    const xsk_gpu_desc* descs;
+    uint8_t* verdicts;
+    xsk_gpu_rec* recs;
+    xsk_gpu_stats* stats;
+    uint32_t opts;
+};
+
+__device__ __forceinline__ uint32_t ld_sys(const volatile uint32_t* p) {
+    return __hip_atomic_load((uint32_t*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(volatile uint32_t* p, uint32_t v) {
+    __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool WIRE>
+__global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
+    __shared__ Echo6Smem<kLLTPW, WIRE, kShip6Stream> sm;
+    __shared__ uint32_t s_cmd[3];  // work?, n, recs
+    xsk_gpu__bell* bell = L.bell;
+    uint32_t served = 0;
+    if (threadIdx.x == 0) {
+        served = ld_sys(&bell->done);  // a previous instance's last batch (stream order: it has exited)
+        st_sys(&bell->alive, 1u);
+    }
+    while (true) {
+        if (threadIdx.x == 0) {
+            uint32_t work = 0, n = 0, recs = 0;
+            uint64_t t0 = wall_clock64();
+            while (true) {
+                const uint32_t seq = ld_sys(&bell->seq);
+                if (seq != served) {
+                    n = ld_sys(&bell->n);
+                    recs = ld_sys(&bell->recs);
+                    served = seq;
+                    work = 1;
+                    break;
+                }
+                if (ld_sys(&bell->stop)) break;
+                if (wall_clock64() - t0 > kIdleTicks) {
+                    // leaving: clear `alive`, then look once more (the host posts, then reads `alive`)
+                    __hip_atomic_store((uint32_t*)&bell->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+                    const uint32_t s2 = __hip_atomic_load((uint32_t*)&bell->seq, __ATOMIC_SEQ_CST,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (s2 == served || ld_sys(&bell->stop)) break;
+                    st_sys(&bell->alive, 1u);
+                    t0 = wall_clock64();
+                    continue;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (n > (uint32_t)XSK_GPU_LOWLAT_MAX) n = XSK_GPU_LOWLAT_MAX;  // the host never posts more
+            s_cmd[0] = work;
+            s_cmd[1] = n;
+            s_cmd[2] = recs;
+        }
+        __syncthreads();
+        const uint32_t work = s_cmd[0], n = s_cmd[1], recs = s_cmd[2];
+        if (!work) break;  // workgroup-uniform
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: fresh descriptors and frames
+        EchoArgs a;
+        a.umem = L.umem;
+        a.umem_size = L.umem_size;
+        a.descs = L.descs;
+        a.n = n;
+        a.verdicts = L.verdicts;
+        a.recs = recs ? L.recs : nullptr;
+        a.partials = nullptr;
+        a.opts = L.opts;
+        a.stats_direct = (unsigned long long*)&L.stats->rx_packets;  // zeroed by the host before posting
+        a.stats_plain = 1;                                            // the only writer
+        const uint32_t ntiles = (n + kTile - 1) / kTile;
+        if (ntiles)
+            echo6_body<kShip6U, kLLTPW, kLLSync, kShip6Stream, false, false, WIRE, false, false, !WIRE && kShip6Mid,
+                       kShip6D2 && !WIRE, kShip6Skm && !WIRE>(a, 0u, ntiles, ntiles, sm);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's stores are performed
+        __syncthreads();
+        if (threadIdx.x == 0) st_sys(&bell->done, served);
+    }
+}
+
+}  // namespace
+
+struct xsk_gpu__lowlat {
+    int device;
+    hipStream_t stream;
+    xsk_gpu__bell* h_bell;
+    xsk_gpu__bell* d_bell;
+    LowlatArgs args;
+    struct xsk_gpu_desc* h_descs;
+    uint8_t* h_verd;
+    struct xsk_gpu_rec* h_recs;
+    struct xsk_gpu_stats* h_stats;
+    int launched;  // a kernel instance was launched and may still run
+};
+
+static int ll_launch(xsk_gpu__lowlat* ll) {
+    ll->h_bell->stop = 0;
+    if (ll->args.opts)
+        hipLaunchKernelGGL(lowlat_kernel<true>, dim3(1), dim3(kThreads6), 0, ll->stream, ll->args);
+    else
+        hipLaunchKernelGGL(lowlat_kernel<false>, dim3(1), dim3(kThreads6), 0, ll->stream, ll->args);
+    HIP_TRY(hipGetLastError());
+    ll->launched = 1;
+    return 0;
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+extern "C" {
+
+void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll) {
+    if (!ll) return;
+    (void)hipSetDevice(ll->device);
+    if (ll->launched) {
+        __atomic_store_n(&ll->h_bell->stop, 1u, __ATOMIC_SEQ_CST);
+        (void)hipStreamSynchronize(ll->stream);  // the kernel sees `stop` within one poll
+        ll->launched = 0;
+    }
+}
+
+static void ll_free(xsk_gpu__lowlat* ll) {
+    if (!ll) return;
+    xsk_gpu__lowlat_stop(ll);
+    if (ll->stream) (void)hipStreamDestroy(ll->stream);
+    if (ll->h_bell) (void)hipHostFree(ll->h_bell);
+    if (ll->h_descs) (void)hipHostFree(ll->h_descs);
+    if (ll->h_verd) (void)hipHostFree(ll->h_verd);
+    if (ll->h_recs) (void)hipHostFree(ll->h_recs);
+    if (ll->h_stats) (void)hipHostFree(ll->h_stats);
+    free(ll);
+}
+
+int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_size, uint32_t opts) {
+    if (!out || !d_umem || (umem_size >> 48) || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
+    *out = nullptr;
+    xsk_gpu__lowlat* ll = (xsk_gpu__lowlat*)calloc(1, sizeof *ll);
+    if (!ll) return -ENOMEM;
+    int rc = 0;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;  // fine-grained: polled across PCIe
+#define LL_TRY(expr)                         \
+    do {                                     \
+        const hipError_t e_ = (expr);        \
+        if (e_ != hipSuccess) {              \
+            rc = xsk_gpu__hip_fail(e_);      \
+            ll_free(ll);                     \
+            return rc;                       \
+        }                                    \
+    } while (0)
+    LL_TRY(hipGetDevice(&ll->device));
+    // a non-blocking stream of its own at the highest priority: the resident kernel neither orders the
+    // null stream nor shares a hardware queue with the context's launch streams
+    int lo = 0, hi = 0;
+    LL_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    LL_TRY(hipStreamCreateWithPriority(&ll->stream, hipStreamNonBlocking, hi));
+    LL_TRY(hipHostMalloc((void**)&ll->h_bell, sizeof(xsk_gpu__bell), fl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_desc), fl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, fl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), fl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_stats, sizeof(struct xsk_gpu_stats), fl));
+    memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
+    LowlatArgs& A = ll->args;
+    LL_TRY(hipHostGetDevicePointer((void**)&A.bell, ll->h_bell, 0));
+    LL_TRY(hipHostGetDevicePointer((void**)&A.descs, ll->h_descs, 0));
+    LL_TRY(hipHostGetDevicePointer((void**)&A.verdicts, ll->h_verd, 0));
+    LL_TRY(hipHostGetDevicePointer((void**)&A.recs, ll->h_recs, 0));
+    LL_TRY(hipHostGetDevicePointer((void**)&A.stats, ll->h_stats, 0));
+#undef LL_TRY
+    A.umem = (uint8_t*)d_umem;
+    A.umem_size = umem_size;
+    A.opts = opts;
+    *out = ll;
+    return 0;  // the kernel starts with the first batch
+}
+
+int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts) {
+    if (!ll || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
+    if (opts == ll->args.opts) return 0;
+    xsk_gpu__lowlat_stop(ll);  // the next batch launches the kernel of the new mode
+    ll->args.opts = opts;
+    return 0;
+}
+
+int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
+    if (!ll || n > XSK_GPU_LOWLAT_MAX) return -EINVAL;
+    xsk_gpu__bell* b = ll->h_bell;
+    int fresh = 0;  // a kernel launched by this call: it reads `done` at start and serves the new seq
+    if (!ll->launched || !__atomic_load_n(&b->alive, __ATOMIC_SEQ_CST)) {
+        // gone (idle exit) or never started: launch; stream order puts it behind an exiting instance
+        const int rc = ll_launch(ll);
+        if (rc) return rc;
+        fresh = 1;
+    }
+    memset(ll->h_stats, 0, sizeof *ll->h_stats);
+    const uint32_t seq = b->seq + 1u;
+    b->n = n;
+    b->recs = want_recs ? 1u : 0u;
+    __atomic_store_n(&b->seq, seq, __ATOMIC_SEQ_CST);  // descriptors and counters are written before this
+    if (!fresh && !__atomic_load_n(&b->alive, __ATOMIC_SEQ_CST)) {
+        // the kernel was leaving (Dekker: it re-reads seq after clearing alive, or this launch serves it)
+        const int rc = ll_launch(ll);
+        if (rc) return rc;
+    }
+    // spin on completion; past 200 us check the kernel is still there, past 2 s give up
+    double t0 = 0.0, tq = 0.0;
+    for (uint32_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) break;
+        if ((spin & 1023u) == 1023u) {
+            const double t = now_s();
+            if (t0 == 0.0) t0 = tq = t;
+            if (t - tq > 2e-4) {
+                tq = t;
+                if (hipStreamQuery(ll->stream) == hipSuccess && __atomic_load_n(&b->done, __ATOMIC_ACQUIRE) != seq) {
+                    const int rc = ll_launch(ll);  // exited without serving the batch: serve it now
+                    if (rc) return rc;
+                }
+            }
+            if (t - t0 > 2.0) return -ETIMEDOUT;
+        }
+        __builtin_ia32_pause();
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return 0;
+}
+
+struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll) { return ll->h_descs; }
+uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll) { return ll->h_verd; }
+struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll) { return ll->h_recs; }
+struct xsk_gpu_stats* xsk_gpu__lowlat_stats(xsk_gpu__lowlat* ll) { return ll->h_stats; }
+
+void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll) { ll_free(ll); }
+
+}  // extern "C"
