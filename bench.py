@@ -263,6 +263,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also measure the PCIe-inclusive rate")
     ap.add_argument("--pool-cap", type=int, default=0, help="cap the batch pool (rehearsals on a shared GPU)")
+    ap.add_argument("--alloc", default="slab", choices=("slab", "separate"),
+                    help="batch pool as one device allocation (slab, like one UMEM region) or one per batch")
     ap.add_argument("--opts", type=int, default=0,
                     help="wire-format options (XSK_GPU_OPT_*, xsk_gpu_echo_dev_opts); 0 = the reference's gates")
     args = ap.parse_args()
@@ -299,8 +301,13 @@ def main():
         + (" (re-arm inside timed loop)" if rearm_in_loop else ""))
     umems, descss = [], []
     t0 = time.perf_counter()
+    # one allocation for the whole pool (the UMEM is one region in an AF_XDP client); separately
+    # allocated 4 GiB batches land on increasingly fragmented physical memory and read up to 10 %
+    # slower late in the pool
+    slab = torch.empty(pool * batch_bytes, dtype=torch.uint8, device=dev) if args.alloc == "slab" else None
     for b in range(pool):
-        u = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
+        u = slab[b * batch_bytes:(b + 1) * batch_bytes] if slab is not None else \
+            torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
         d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
         # round-robin shard: local frame j of batch b is global frame first + j*step
         first, gstep = shard.shard_range(b, n, rank, world)
@@ -404,7 +411,7 @@ def main():
                     "to oracle/echo_oracle.c)",
             "config": {"workload": desc, "frames_per_gpu": n, "frame_len": [lo, hi], "stride": stride,
                        "frame_bytes_per_gpu_step": frame_bytes, "parallelism": f"shard{world}:round-robin",
-                       "layout": "device-resident UMEM slab + xdp_desc array",
+                       "layout": "device-resident UMEM slab + xdp_desc array", "pool_alloc": args.alloc,
                        "rearm_in_timed_region": rearm_in_loop},
             "verified": bool(ok_all == world),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

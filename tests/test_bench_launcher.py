@@ -25,6 +25,12 @@ def test_launcher_spawns_n_ranks(monkeypatch):
         return subprocess.CompletedProcess(cmd, 7)
 
     monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    import xsknet_amd
+
+    def no_gpu(*a, **k):
+        raise AssertionError("the launcher must not load the HIP library")
+
+    monkeypatch.setattr(xsknet_amd, "lib", no_gpu)
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5", "--config", "c5"])
     with pytest.raises(SystemExit) as e:
@@ -35,8 +41,6 @@ def test_launcher_spawns_n_ranks(monkeypatch):
     assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "--master-addr=127.0.0.1" in cmd
     assert cmd[-6:] == ["--gpus", "8", "--steps", "5", "--config", "c5"]
     assert os.path.samefile(cmd[-7], os.path.join(ROOT, "bench.py"))
-    # the launcher never touched the GPU runtime
-    assert "xsknet_amd" not in sys.modules or not getattr(sys.modules["xsknet_amd"], "_lib", None)
 
 
 def test_rank_refuses_world_size_mismatch(monkeypatch):

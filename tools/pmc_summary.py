@@ -20,7 +20,7 @@ KERNEL = "echo_kernel"
 
 
 def per_launch(d, counter):
-    f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter and KERNEL in r["Kernel_Name"]]
     name = re.search(r"echo_kernel\d<[^>]*>", rows[0]["Kernel_Name"]).group(0)
     return statistics.median(float(r["Counter_Value"]) for r in rows), len(rows), name

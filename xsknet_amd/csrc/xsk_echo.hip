@@ -150,7 +150,19 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     const uint32_t ncu = xsk_gpu__num_cu(device);
     if (!ncu) return xsk_gpu__hip_fail(hipErrorInvalidDevice);
     uint32_t grid = 0, tiles_per_wg = 0;
-    echo6_geometry(n, ncu, &grid, &tiles_per_wg);
+    // a small batch (the RX loop's) runs on ONE workgroup as sub-tiles of ceil(n / 16) frames, so all 16
+    // waves share it: over PCIe (zerocopy host UMEM) one wave alone would stream its 64 frames with only
+    // its own loads in flight
+    const bool small = n <= (uint32_t)XSK_GPU_LOWLAT_MAX;
+    uint32_t tl = kTile;
+    if (small) {
+        tl = ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
+        tl = tl < 4u ? 4u : (tl > (uint32_t)kTile ? (uint32_t)kTile : tl);
+        grid = 1;
+        tiles_per_wg = (n + tl - 1) / tl;
+    } else {
+        echo6_geometry(n, ncu, &grid, &tiles_per_wg);
+    }
     const hipStream_t s = (hipStream_t)stream;
     EchoArgs args;
     args.umem = (uint8_t*)d_umem;
@@ -161,6 +173,7 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     args.recs = d_recs;
     args.partials = nullptr;
     args.opts = opts;
+    args.tile_live = tl;
     bool fold = false;
     if (d_stats) {
         if (!hoststats) {
@@ -174,12 +187,18 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
         }
     }
     const int slot = timer_begin(device, s);
-    if (opts == 0)
+    if (opts == 0 && !small)
         echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2,
                      kShip6Skm><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    else  // wire mode: 128-B windows, one tile per wave per round
+    else if (opts == 0)  // one round of sub-tiles, writes as soon as a wave has read
+        echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2, kShip6Skm,
+                     true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+    else if (!small)  // wire mode: 128-B windows, one tile per wave per round
         echo_kernel6<kShip6U, 1, kShip6Sync, kShip6Stream, false, false, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(
             args, tiles_per_wg);
+    else
+        echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, true, false, false, false, false, false, true>
+            <<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     const hipError_t le = hipGetLastError();
     timer_end(slot, s);
     if (le != hipSuccess) return xsk_gpu__hip_fail(le);

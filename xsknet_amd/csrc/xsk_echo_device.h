@@ -35,6 +35,10 @@ struct EchoArgs {
     // device-scope atomics, or -- stats_plain, a one-workgroup launch on mapped host memory -- plain adds
     unsigned long long* stats_direct = nullptr;  // &stats->rx_packets (4 consecutive u64)
     uint32_t stats_plain = 0;
+    // SUBT kernels only: live frames per 64-lane tile (a multiple of 4, <= 64); tile t holds frames
+    // [t * tile_live, t * tile_live + tile_live) in lanes 0 .. tile_live - 1 -- a small batch spreads over
+    // more waves (the low-latency kernel: a 64-frame batch is 16 tiles of 4 frames, one per wave)
+    uint32_t tile_live = 64;
 };
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -860,7 +864,7 @@ struct Echo6Smem {
 // the counters (store_partials).  echo_kernel6 runs it once per workgroup on its static share; the
 // low-latency persistent kernel (xsk_lowlat.hip) once per doorbell.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false>
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -912,7 +916,9 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             asm volatile("" : "+v"(lane));
             uint8_t* rows = s_hdr[wave][i];
             const uint32_t q = lane >> 4, k = lane & 15u;
-            const uint32_t fi = t * kTile + lane;
+            static_assert(!(SUBT && PF), "sub-tiles take no descriptor prefetch");
+            const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
+            const bool in_n = (!SUBT || lane < a.tile_live) && fi < a.n;  // a live frame of the batch
             // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
             u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
             if (PF) {
@@ -921,7 +927,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 const uint32_t fn = tn * kTile + lane;
                 dnext = u32x4{0u, 0u, 0u, 0u};
                 if (tn < t_end && fn < a.n) dnext = *(const u32x4*)(a.descs + fn);
-            } else if (fi < a.n) {
+            } else if (in_n) {
                 dsc = *(const u32x4*)(a.descs + fi);
             }
             const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
@@ -929,7 +935,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             // reference mode reads bytes [0, 38) whenever len >= 20 (xsk_receive.c:120-157); wire mode
             // reads only [addr, addr + len) plus the window
             const uint64_t need = WIRE ? len : (len >= 20 ? (len > 38 ? len : 38) : len);
-            const bool ok = fi < a.n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+            const bool ok = in_n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
             const bool parse = ok && len >= (WIRE ? 14u : 20u);
             const uint64_t a16 = addr & ~15ull;
             const uint32_t off = (uint32_t)addr & 15u;
@@ -961,7 +967,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             }
             alo[i] = dsc.x;
             ahi[i] = dsc.y;
-            if (SYNC == 2) round_bytes += wave_sum_u32(fi < a.n ? min(len, 65536u) : 0u);
+            if (SYNC == 2) round_bytes += wave_sum_u32(in_n ? min(len, 65536u) : 0u);
 
             // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
             if (__ballot(nit != 0u) != 0ull) {
@@ -1098,10 +1104,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
             bool wb;
             if (WIRE)
-                wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, fi < a.n, wend, cnt, &rec[i],
+                wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec[i],
                                        &verd[i]);
             else
-                wb = header_phase5<true, STREAM >= 1, D2>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, fi < a.n, ok,
+                wb = header_phase5<true, STREAM >= 1, D2>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, in_n, ok,
                                                        parse, fi, cnt, &rec[i], &verd[i]);
             wbm[i] = __ballot(wb);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1155,8 +1161,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     }
                 }
             }
-            const uint32_t fi = t * kTile + lane;
-            if (fi < a.n) {
+            const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
+            if ((!SUBT || lane < a.tile_live) && fi < a.n) {
                 if (a.recs) {
                     if (NTS) __builtin_nontemporal_store(rec[i], (u32x4*)a.recs + fi);
                     else ((u32x4*)a.recs)[fi] = rec[i];
@@ -1188,14 +1194,17 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 }
 
 // One 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg tiles (echo6_geometry).
+// SUBT: tiles of a.tile_live frames (small batches, one workgroup).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false>
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
-    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
+    const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM>(a, t_begin, t_end, tiles_per_wg, sm);
+    echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT>(a, t_begin, t_end, tiles_per_wg,
+                                                                                   sm);
 }
 
 

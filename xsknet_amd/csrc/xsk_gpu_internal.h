@@ -35,17 +35,19 @@ XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
  * layout (mapped, fine-grained pinned host memory): host-written and device-written words live on
  * separate 128-byte lines. */
 struct xsk_gpu__bell {
-    /* host -> device */
-    volatile uint32_t seq;   /* bumped by one per posted batch                               */
-    volatile uint32_t n;     /* frames of the posted batch (<= XSK_GPU_LOWLAT_MAX)             */
-    volatile uint32_t recs;  /* nonzero: write records                                        */
-    volatile uint32_t stop;  /* nonzero: the persistent kernel exits at its next poll          */
-    uint32_t pad0[28];
+    /* host -> device: ONE 64-bit word, so a poll is one PCIe read:
+     *   bits 0-31 seq (bumped by one per posted batch), 32-47 n (<= XSK_GPU_LOWLAT_MAX),
+     *   bit 48 write records, bit 63 stop (the persistent kernel exits at its next poll) */
+    volatile uint64_t cmd;
+    uint32_t pad0[30];
     /* device -> host */
     volatile uint32_t done;  /* seq of the last completed batch                               */
     volatile uint32_t alive; /* 1 while the persistent kernel runs                            */
     uint32_t pad1[30];
 };
+#define XSK_GPU__BELL_N(n) ((uint64_t)(n) << 32)
+#define XSK_GPU__BELL_RECS (1ull << 48)
+#define XSK_GPU__BELL_STOP (1ull << 63)
 
 typedef struct xsk_gpu__lowlat xsk_gpu__lowlat;
 /* Create the channel on the current device for the (mapped) UMEM alias d_umem: its doorbell, mapped

@@ -52,6 +52,9 @@ struct LowlatArgs {
 __device__ __forceinline__ uint32_t ld_sys(const volatile uint32_t* p) {
     return __hip_atomic_load((uint32_t*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ uint64_t ld_sys64(const volatile uint64_t* p) {
+    return __hip_atomic_load((uint64_t*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void st_sys(volatile uint32_t* p, uint32_t v) {
     __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -71,21 +74,21 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             uint32_t work = 0, n = 0, recs = 0;
             uint64_t t0 = wall_clock64();
             while (true) {
-                const uint32_t seq = ld_sys(&bell->seq);
-                if (seq != served) {
-                    n = ld_sys(&bell->n);
-                    recs = ld_sys(&bell->recs);
-                    served = seq;
+                const uint64_t c = ld_sys64(&bell->cmd);  // one PCIe read per poll
+                if ((uint32_t)c != served) {
+                    n = (uint32_t)(c >> 32) & 0xFFFFu;
+                    recs = (uint32_t)(c >> 48) & 1u;
+                    served = (uint32_t)c;
                     work = 1;
                     break;
                 }
-                if (ld_sys(&bell->stop)) break;
+                if (c & XSK_GPU__BELL_STOP) break;
                 if (wall_clock64() - t0 > kIdleTicks) {
                     // leaving: clear `alive`, then look once more (the host posts, then reads `alive`)
                     __hip_atomic_store((uint32_t*)&bell->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-                    const uint32_t s2 = __hip_atomic_load((uint32_t*)&bell->seq, __ATOMIC_SEQ_CST,
+                    const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
                                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (s2 == served || ld_sys(&bell->stop)) break;
+                    if ((uint32_t)c2 == served || (c2 & XSK_GPU__BELL_STOP)) break;
                     st_sys(&bell->alive, 1u);
                     t0 = wall_clock64();
                     continue;
@@ -112,10 +115,15 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         a.opts = L.opts;
         a.stats_direct = (unsigned long long*)&L.stats->rx_packets;  // zeroed by the host before posting
         a.stats_plain = 1;                                            // the only writer
-        const uint32_t ntiles = (n + kTile - 1) / kTile;
+        // spread the batch over all 16 waves: tiles of ceil(n / 16) frames (a multiple of 4: one 16-lane
+        // row per frame and step), so a 64-frame batch is 16 tiles of 4 frames, each wave one step
+        uint32_t tl = ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
+        tl = tl < 4u ? 4u : (tl > (uint32_t)kTile ? (uint32_t)kTile : tl);
+        a.tile_live = tl;
+        const uint32_t ntiles = (n + tl - 1) / tl;
         if (ntiles)
             echo6_body<kShip6U, kLLTPW, kLLSync, kShip6Stream, false, false, WIRE, false, false, !WIRE && kShip6Mid,
-                       kShip6D2 && !WIRE, kShip6Skm && !WIRE>(a, 0u, ntiles, ntiles, sm);
+                       kShip6D2 && !WIRE, kShip6Skm && !WIRE, true>(a, 0u, ntiles, ntiles, sm);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's stores are performed
         __syncthreads();
         if (threadIdx.x == 0) st_sys(&bell->done, served);
@@ -135,10 +143,11 @@ struct xsk_gpu__lowlat {
     struct xsk_gpu_rec* h_recs;
     struct xsk_gpu_stats* h_stats;
     int launched;  // a kernel instance was launched and may still run
+    uint32_t seq;  // last posted batch
 };
 
 static int ll_launch(xsk_gpu__lowlat* ll) {
-    ll->h_bell->stop = 0;
+    __atomic_store_n(&ll->h_bell->cmd, (uint64_t)ll->seq, __ATOMIC_SEQ_CST);  // clears a stop request
     if (ll->args.opts)
         hipLaunchKernelGGL(lowlat_kernel<true>, dim3(1), dim3(kThreads6), 0, ll->stream, ll->args);
     else
@@ -160,7 +169,7 @@ void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll) {
     if (!ll) return;
     (void)hipSetDevice(ll->device);
     if (ll->launched) {
-        __atomic_store_n(&ll->h_bell->stop, 1u, __ATOMIC_SEQ_CST);
+        __atomic_store_n(&ll->h_bell->cmd, (uint64_t)ll->seq | XSK_GPU__BELL_STOP, __ATOMIC_SEQ_CST);
         (void)hipStreamSynchronize(ll->stream);  // the kernel sees `stop` within one poll
         ll->launched = 0;
     }
@@ -239,10 +248,11 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
         fresh = 1;
     }
     memset(ll->h_stats, 0, sizeof *ll->h_stats);
-    const uint32_t seq = b->seq + 1u;
-    b->n = n;
-    b->recs = want_recs ? 1u : 0u;
-    __atomic_store_n(&b->seq, seq, __ATOMIC_SEQ_CST);  // descriptors and counters are written before this
+    const uint32_t seq = ll->seq + 1u;
+    ll->seq = seq;
+    // descriptors and zeroed counters are written before this one store
+    __atomic_store_n(&b->cmd, (uint64_t)seq | XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull),
+                     __ATOMIC_SEQ_CST);
     if (!fresh && !__atomic_load_n(&b->alive, __ATOMIC_SEQ_CST)) {
         // the kernel was leaving (Dekker: it re-reads seq after clearing alive, or this launch serves it)
         const int rc = ll_launch(ll);
