@@ -147,9 +147,11 @@ def test_tuning_code_is_not_in_the_product_library():
     for sym in ("xsk_gpu__echo_variant", "xsk_gpu__echo_wire_variant", "xsk_gpu__set_stats_atomic",
                 "xsk_gpu__set_wire_impl", "echo_wire_kernel", "echo_kernel5", "echo_kernel7"):
         assert sym not in prod, sym
-    # the product exports the C ABI, plus one internal helper the tuning library links against
+    # the product exports the C ABI, plus the CU count the tuning library links against and a
+    # diagnostics hook of the LOWLAT channel (tools/echo_replay)
     exported = set(re.findall(r"\bT (\w+)", prod))
-    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu"}, exported - set(declared_functions())
+    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu", "xsk_gpu__lowlat_trace"}, \
+        exported - set(declared_functions())
     tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
                           check=True).stdout
     assert "xsk_gpu__echo_variant" in tune and "xsk_gpu__echo_wire_variant" in tune

@@ -428,7 +428,7 @@ def test_timing_hook():
     assert cnt == 3 and ms > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96])
 @pytest.mark.parametrize("grid", [0, 1, 7])
 @pytest.mark.parametrize("len_hi", [2048, 112, 48])
 def test_kernel_variants_parity(variant, grid, len_hi):
@@ -449,7 +449,7 @@ def test_kernel_variants_parity(variant, grid, len_hi):
     d_umem, d_descs = to_dev(umem), to_dev(descs)
     d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
     d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    ws = torch.zeros(1 << 16, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)  # 93-95: queue counters at +768 KiB
     rc = L.xsk_gpu__echo_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
                                  d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
                                  torch.cuda.current_stream().cuda_stream)
@@ -458,6 +458,39 @@ def test_kernel_variants_parity(variant, grid, len_hi):
     assert (d_verd.cpu().numpy() == v_ref).all()
     assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
     assert (d_umem.cpu().numpy() == ref).all()
+    if variant in (93, 95):  # the dynamic schedule leaves its queue counters zeroed for the next launch
+        assert int(ws[768 << 10:(768 << 10) + 36].sum().item()) == 0
+
+
+def test_dynamic_schedule_full_size_and_reuse():
+    """The dynamic round schedule (tuning variants 93 / 95) over 1 M mixed frames, three launches on one
+    workspace: every frame exact each time (the counters reset themselves between launches)."""
+    L = X.tune_lib()
+    dev = _dev()
+    n, stride = 1 << 20, 2048
+    for variant in (93, 95):
+        d_umem = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
+        d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        X.synth_dev(d_umem, d_descs, n, 0, stride, 0x5EED9393, 0, 1, 0, 64, 1500)
+        before = d_umem.clone()
+        host = np.zeros(n * stride, np.uint8)
+        descs = oracle.synth_batch(host, n, 0, stride, 0x5EED9393, 0, 1, 0, 64, 1500, threads=_threads())
+        v_ref, r_ref, _ = oracle.echo_batch(host, descs, threads=_threads())
+        d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+        d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+        for rep in range(3):
+            if rep:
+                d_umem.copy_(before)
+            rc = L.xsk_gpu__echo_variant(variant, 0, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                         d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                         torch.cuda.current_stream().cuda_stream)
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert (d_verd.cpu().numpy() == v_ref).all()
+            assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+            assert (d_umem.cpu().numpy() == host).all(), (variant, rep)
+        del d_umem, before
 
 
 def test_staged_pipeline_multi_chunk():

@@ -10,6 +10,7 @@ UMEM (untimed) so every call transforms echo requests.  Prints one JSON line per
                           [--gpus 0,0] [--reps 200]
 """
 import argparse
+import itertools
 import json
 import os
 import subprocess
@@ -23,6 +24,29 @@ import numpy as np  # noqa: E402
 import oracle  # noqa: E402  (frame generator only)
 
 
+def run_one(exe, p, flen, mode, batch, tile, args):
+    cmd = [exe, p("u"), p("d"), p("o"), p("v"), str(batch), mode, f"reps={args.reps}"]
+    if args.gpus:
+        cmd.insert(7, f"gpus={args.gpus}")
+    env = dict(os.environ, XSK_GPU_LOWLAT_TILE=tile) if tile else None
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0:
+        print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "error": r.stderr[-300:]}))
+        sys.exit(1)
+    kv = dict(x.split("=") for x in r.stdout.split())
+    us = float(kv["us_per_call"])
+    rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto",
+           "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3), "calls": int(kv["calls"])}
+    if "trace_ns" in kv:  # LOWLAT: the last batch's phases on the GPU
+        t = [int(x) for x in kv["trace_ns"].split(",")]
+        rec["last_batch_gpu_us"] = {
+            "poll_period": t[0] / 1e3, "acquire": t[1] / 1e3, "transform": t[2] / 1e3, "release": t[3] / 1e3,
+            "wave0_in_transform": {"descriptors": t[4] / 1e3, "streamed": t[5] / 1e3, "header_phase": t[6] / 1e3,
+                                   "writes_issued": t[7] / 1e3, "counters": t[8] / 1e3},
+            "shader_clock_mhz": t[9], "host_before_doorbell": t[10] / 1e3, "host_doorbell_to_done": t[11] / 1e3}
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lens", default="64,1500")
@@ -30,6 +54,7 @@ def main():
     ap.add_argument("--batches", default="64,256,1024,4096")
     ap.add_argument("--gpus", default="")
     ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--tiles", default="", help="LOWLAT frames per wave to sweep (XSK_GPU_LOWLAT_TILE), e.g. 4,16,64")
     args = ap.parse_args()
     exe = os.path.join(ROOT, "tools", "echo_replay")
     n, chunk = 4096, 4096
@@ -40,20 +65,10 @@ def main():
             descs = oracle.synth_batch(umem, n, 256, chunk, seed=0x5EED0001, mode=0, len_lo=flen, len_hi=flen)
             umem.tofile(p("u"))
             descs.tofile(p("d"))
-            for mode in args.modes.split(","):
-                for batch in (int(x) for x in args.batches.split(",")):
-                    cmd = [exe, p("u"), p("d"), p("o"), p("v"), str(batch), mode, f"reps={args.reps}"]
-                    if args.gpus:
-                        cmd.insert(7, f"gpus={args.gpus}")
-                    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
-                    if r.returncode != 0:
-                        print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "error": r.stderr[-300:]}))
-                        sys.exit(1)
-                    kv = dict(x.split("=") for x in r.stdout.split())
-                    us = float(kv["us_per_call"])
-                    print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0",
-                                      "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3),
-                                      "calls": int(kv["calls"])}), flush=True)
+            for mode, batch in itertools.product(args.modes.split(","), (int(x) for x in args.batches.split(","))):
+                for tile in (args.tiles.split(",") if args.tiles and mode == "lowlat" else [""]):
+                    rec = run_one(exe, p, flen, mode, batch, tile, args)
+                    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

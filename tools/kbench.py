@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--grids", default="0")  # 0 = library default; comma list of caps, -1 = full grid
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pool", type=int, default=1)
+    ap.add_argument("--slab", action="store_true", help="the pool's batches in one allocation")
+    ap.add_argument("--no-recs", action="store_true", help="pass no record buffer (records are optional)")
     args = ap.parse_args()
     L = X.tune_lib()
     dev = torch.device("cuda:0")
@@ -52,8 +54,10 @@ def main():
         free, _ = torch.cuda.mem_get_info(dev)
         pool = max(1, min(args.pool, int(free * 0.8) // (n * stride + n * 16)))
         umems, descss = [], []
+        slab = torch.empty(pool * n * stride, dtype=torch.uint8, device=dev) if args.slab else None
         for b in range(pool):
-            u = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+            u = slab[b * n * stride:(b + 1) * n * stride] if slab is not None else \
+                torch.empty(n * stride, dtype=torch.uint8, device=dev)
             d = torch.empty(n * 16, dtype=torch.uint8, device=dev)
             X.synth_dev(u, d, n, 0, stride, 0x5EED0003, b * n, 1, 0, lo, hi)
             if lname.startswith("c4ramp"):  # equal bytes per tile, ragged inside (mean 782 B)
@@ -82,7 +86,7 @@ def main():
                         else:
                             rc = L.xsk_gpu__echo_variant(v, maxg, umems[b].data_ptr(), n * stride,
                                                          descss[b].data_ptr(), n, verds[b].data_ptr(),
-                                                         recs.data_ptr(), ws.data_ptr(), sp)
+                                                         None if args.no_recs else recs.data_ptr(), ws.data_ptr(), sp)
                             assert rc == 0, rc
                         ev1.record()
                         evs.append((ev0, ev1))
@@ -92,12 +96,15 @@ def main():
                     if rep > 0:
                         times[(v, g)].extend(evs)
             torch.cuda.synchronize()
-        if 79 in variants:  # per-workgroup start/end wall clock of the last launch (workspace tail)
+        for wv in [v for v in variants if v in (79, 94)]:  # per-workgroup start/end wall clock (workspace tail)
+            torch.cuda.synchronize()  # batch wv's launch reads is a request batch (every sweep re-arms)
+            assert L.xsk_gpu__echo_variant(wv, 0, umems[0].data_ptr(), n * stride, descss[0].data_ptr(), n,
+                                           verds[0].data_ptr(), recs.data_ptr(), ws.data_ptr(), sp) == 0
             torch.cuda.synchronize()
             t = ws.view(torch.int64)[8192:8192 + 2 * 256].cpu().view(256, 2).double() / 100.0  # us
             t0 = t[:, 0].min()
             st, en = t[:, 0] - t0, t[:, 1] - t0
-            print(json.dumps({"layout": lname, "wg_timing": True, "start_max": round(float(st.max()), 1),
+            print(json.dumps({"layout": lname, "wg_timing": True, "variant": wv, "start_max": round(float(st.max()), 1),
                               "end_min": round(float(en.min()), 1), "end_med": round(float(en.median()), 1),
                               "end_max": round(float(en.max()), 1),
                               "end_mean_per_xcd": [round(float(en[x::8].mean()), 1) for x in range(8)],
@@ -110,7 +117,7 @@ def main():
             print(json.dumps({"layout": lname, "pool": pool, "variant": v, "grid": g, "us_med": round(med * 1e3, 2),
                               "us_min": round(ms[0] * 1e3, 2), "gbs_med": round(nb / (med / 1e3) / 1e9, 1),
                               "mframes_s": round(n / (med / 1e3) / 1e6, 1)}), flush=True)
-        del umems, descss, verds, recs
+        del umems, descss, verds, recs, slab
         torch.cuda.empty_cache()
 
 

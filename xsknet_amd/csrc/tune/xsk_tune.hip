@@ -351,6 +351,10 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         uint32_t g6 = 0, per = 0;
         echo6_geometry(n, max_grid ? max_grid : xsk_gpu__num_cu(device), &g6, &per);
         const dim3 gg(g6), bb(kThreads6);
+        if (variant >= 93 && variant <= 95) {  // queue counters at workspace + 768 KiB: zero, left zero
+            if (!d_workspace) return -EINVAL;
+            args.queue = (uint32_t*)((uint8_t*)d_workspace + (768u << 10));
+        }
         if (variant == 90 || variant == 91) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
             if (!d_workspace) return -EINVAL;
             HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
@@ -386,6 +390,15 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 90: echo_kernel6<4, 2, 3, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 91: echo_kernel6<4, 2, 4, 2, false, false, false, false, false, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 92: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 93-95: the dynamic round schedule (per-XCD regions, atomic claims, stealing); 94 + WGT
+            // end-time probes, 95 with one tile per wave per round
+            case 93: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 94: echo_kernel6<4, 2, 2, 2, false, true, false, false, false, true, true, true, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 95: echo_kernel6<4, 1, 2, 2, false, false, false, false, false, true, true, true, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 96: echo_kernel6<4, 1, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 97 / 98: the shipped kernel with 6 / 8 row-loads in flight per lane (a 1500-B frame in one batch)
+            case 97: echo_kernel6<6, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 98: echo_kernel6<8, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;

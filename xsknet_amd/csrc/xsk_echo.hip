@@ -11,6 +11,7 @@
 #include <mutex>
 
 #include "xsk_echo_device.h"
+#include "xsk_gpu_internal.h"
 #include "xsk_hip_util.h"
 
 using namespace xskgpu;
@@ -132,11 +133,12 @@ uint32_t xsk_gpu__num_cu(int device) {
 
 // One transform launch (reference mode for opts == 0, wire mode otherwise).  Counters: device memory
 // (hoststats == 0) -> every workgroup adds its four counters with device-scope atomics, one launch;
-// mapped host memory (hoststats == 1, the zerocopy host context) -> a one-workgroup launch adds them
-// itself, a larger grid writes per-workgroup partials that a one-workgroup fold launch adds.
+// mapped host memory (hoststats == 1, the zerocopy host context: d_stats is a slot the host zeroed for
+// this call) -> a one-workgroup launch stores them itself, a larger grid writes per-workgroup partials
+// that a one-workgroup fold launch adds.
 static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t opts,
                        uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
-                       void* d_workspace, void* stream, int hoststats) {
+                       void* d_workspace, void* stream, int hoststats, uint32_t tile) {
     if (opts & ~XSK_GPU_OPT_ALL) return -EINVAL;
     if (n == 0) return 0;
     if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
@@ -156,7 +158,7 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     const bool small = n <= (uint32_t)XSK_GPU_LOWLAT_MAX;
     uint32_t tl = kTile;
     if (small) {
-        tl = ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
+        tl = tile ? ((tile + 3u) & ~3u) : ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
         tl = tl < 4u ? 4u : (tl > (uint32_t)kTile ? (uint32_t)kTile : tl);
         grid = 1;
         tiles_per_wg = (n + tl - 1) / tl;
@@ -213,20 +215,21 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
 int xsk_gpu_echo_dev(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                      void* d_workspace, void* stream) {
-    return echo_launch(d_umem, umem_size, d_descs, n, 0, d_verdicts, d_recs, d_stats, d_workspace, stream, 0);
+    return echo_launch(d_umem, umem_size, d_descs, n, 0, d_verdicts, d_recs, d_stats, d_workspace, stream, 0, 0);
 }
 
 int xsk_gpu_echo_dev_opts(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
                           struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream) {
-    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 0);
+    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 0, 0);
 }
 
 // Internal (xsk_gpu_host.c, zerocopy mode): d_stats is mapped pinned host memory -> no device atomics.
 int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                                      uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
-                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream) {
-    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 1);
+                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream, uint32_t tile) {
+    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 1,
+                       tile);
 }
 
 int xsk_gpu_timing_enable(int enable) {

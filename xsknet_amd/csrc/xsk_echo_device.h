@@ -31,14 +31,21 @@ struct EchoArgs {
     xsk_gpu_rec* recs;
     unsigned long long* partials;  // [gridDim.x][4]: rx_packets, rx_bytes, tx_packets, tx_bytes
     uint32_t opts = 0;             // XSK_GPU_OPT_* (wire-mode kernels only)
-    // every workgroup adds its counters straight into the caller's stats (no fold launch):
-    // device-scope atomics, or -- stats_plain, a one-workgroup launch on mapped host memory -- plain adds
+    // every workgroup adds its counters straight into the caller's stats (no fold launch): device-scope
+    // atomics, or -- stats_plain, a one-workgroup launch on a zeroed per-call slot of mapped host memory --
+    // plain stores (no read across PCIe)
     unsigned long long* stats_direct = nullptr;  // &stats->rx_packets (4 consecutive u64)
     uint32_t stats_plain = 0;
     // SUBT kernels only: live frames per 64-lane tile (a multiple of 4, <= 64); tile t holds frames
     // [t * tile_live, t * tile_live + tile_live) in lanes 0 .. tile_live - 1 -- a small batch spreads over
     // more waves (the low-latency kernel: a 64-frame batch is 16 tiles of 4 frames, one per wave)
     uint32_t tile_live = 64;
+    // DYN kernels only: 9 u32 queue counters (per-region heads, exit count), zero on entry and left zero
+    uint32_t* queue = nullptr;
+    // TRACE kernels only: wave 0's wall clock at the body's phase boundaries (diagnostics, 6 x u64)
+    unsigned long long* trace = nullptr;
+    // DLDS kernels only: nonzero = the batch's descriptors (n <= 64) are already in the LDS (Echo6Smem::desc)
+    uint32_t desc_in_lds = 0;
 };
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -81,12 +88,16 @@ __device__ __forceinline__ void store_partials(const EchoArgs& a, Counters c, un
         s_cnt[wave][2] = c.txp;
         s_cnt[wave][3] = c.txb;
     }
-    __syncthreads();
+    // the rows travel through LDS only: wait for the LDS writes, then meet -- not __syncthreads(), whose
+    // workgroup-scope release would first wait for every outstanding global store (a PCIe round trip
+    // when the frames live in mapped host memory)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
     if (threadIdx.x < 4) {
         unsigned long long s = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) s += s_cnt[w][threadIdx.x];
-        if (a.stats_direct && a.stats_plain) a.stats_direct[threadIdx.x] += s;  // sole writer (host memory)
+        if (a.stats_direct && a.stats_plain) a.stats_direct[threadIdx.x] = s;  // sole writer of a zeroed slot
         else if (a.stats_direct)  // every workgroup adds its own: non-returning device-scope atomics
             __hip_atomic_fetch_add(a.stats_direct + threadIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else a.partials[blockIdx.x * 4 + threadIdx.x] = s;
@@ -492,8 +503,7 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
                 if (FAST) {
                     v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(in ? crel + ro : 0x80000000u), 0, kAuxNT);
                 } else {
-                    const u32x4 y = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? ca16 + ro : 0ull)));
-                    v[u] = in ? y : u32x4{0u, 0u, 0u, 0u};
+                    if (in) v[u] = __builtin_nontemporal_load((const u32x4*)(a.umem + ca16 + ro));
                 }
             }
         }
@@ -847,6 +857,67 @@ constexpr uint32_t kHeavyLen = 1024;
 // the header phase's IPv4 sum with fixed masks when every frame has its whole header.
 // SKM: ranked streams mask only slots where a frame ends and rank small-row tiles by counting; uniform
 // short / ping-size tiles compute their ICMP byte masks once per tile.
+// Dynamic round schedule (DYN, tuning): the batch's units of kWaves6 tiles (one tile per wave) are cut
+// into 8 contiguous regions, one per XCD (workgroup g is taken to sit on XCD g % 8 -- a speed heuristic
+// only, nothing depends on it).  A workgroup's first round takes TPW units of its home region statically;
+// later rounds claim TPW consecutive units of the home region with one atomicAdd on the region's head
+// and, once it is exhausted, move on to the next regions in turn (stealing from slower XCDs).  The last
+// workgroup to leave zeroes the counters for the next launch (queue: head[8], exits).  Thread 0 only.
+struct DynQueue {
+    uint32_t* q;
+    uint32_t units, ntiles, home, k, nwg, first;
+    __device__ __forceinline__ void init(const EchoArgs& a, int tpw) {
+        q = a.queue;
+        ntiles = (a.n + kTile - 1) / kTile;
+        units = (ntiles + kWaves6 - 1) / kWaves6;
+        home = blockIdx.x & 7u;
+        k = 0;
+        nwg = gridDim.x;
+        first = 1;
+        (void)tpw;
+    }
+    __device__ __forceinline__ uint32_t rbeg(uint32_t x) const { return (uint32_t)(((uint64_t)units * x) >> 3); }
+    // workgroups whose home region is x
+    __device__ __forceinline__ uint32_t nhome(uint32_t x) const { return nwg > x ? (nwg - x + 7u) >> 3 : 0u; }
+    template <int TPW>
+    __device__ __forceinline__ void claim_round(uint32_t (*out)[2]) {
+        uint32_t u0 = 0, nu = 0;  // claimed units [u0, u0 + nu)
+        if (first) {              // static first round: TPW units of the home region, no atomics
+            first = 0;
+            const uint32_t rb = rbeg(home), re = rbeg(home + 1);
+            const uint32_t b = rb + (blockIdx.x >> 3) * (uint32_t)TPW;
+            if (b < re) {
+                u0 = b;
+                nu = min((uint32_t)TPW, re - b);
+            }
+        }
+        while (!nu && k < 8u) {
+            const uint32_t x = (home + k) & 7u;
+            const uint32_t rb = rbeg(x), re = rbeg(x + 1);
+            const uint32_t ns = min(nhome(x) * (uint32_t)TPW, re - rb);  // units the first round took
+            const uint32_t old = __hip_atomic_fetch_add(q + x, (uint32_t)TPW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t b = rb + ns + old;
+            if (b < re) {
+                u0 = b;
+                nu = min((uint32_t)TPW, re - b);
+            } else {
+                ++k;  // region exhausted for good
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const bool v = (uint32_t)i < nu;
+            out[i][0] = v ? (u0 + (uint32_t)i) * kWaves6 : 0u;
+            out[i][1] = v ? min((u0 + (uint32_t)i + 1u) * kWaves6, ntiles) : 0u;
+        }
+    }
+    __device__ __forceinline__ void leave() {
+        if (__hip_atomic_fetch_add(q + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwg - 1u) {
+            for (int x = 0; x < 9; ++x) __hip_atomic_store(q + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+};
+
 // LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB in reference mode).
 template <int TPW, bool WIRE, int STREAM>
 struct Echo6Smem {
@@ -857,6 +928,8 @@ struct Echo6Smem {
     uint32_t sort[STREAM >= 1 ? kWaves6 : 1][80];                          // 5 KiB (STREAM 1, 2)
     unsigned long long cnt[kWaves6][4];
     uint32_t arrive;
+    uint32_t claim[TPW][2];  // DYN: this round's units [begin, end) in tiles
+    u32x4 desc[kTile];       // DLDS: the descriptors of a batch of <= 64 frames, delivered with its doorbell
 };
 
 // The round kernel's work over the tiles [t_begin, t_end) of one workgroup (every wave of the
@@ -864,9 +937,11 @@ struct Echo6Smem {
 // the counters (store_partials).  echo_kernel6 runs it once per workgroup on its static share; the
 // low-latency persistent kernel (xsk_lowlat.hip) once per doorbell.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false>
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
+          bool DYN = false, bool TRACE = false, bool DLDS = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM>& sm) {
+    static_assert(!DYN || (!PF && SYNC < 3 && !SUBT), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
     const uint64_t wgt_start = WGT ? wall_clock64() : 0ull;
@@ -898,7 +973,31 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     uint32_t* gbar = (SYNC >= 3 && a.partials) ? (uint32_t*)(a.partials + 65536) : nullptr;
     uint32_t gbar_n = 0;
     const uint32_t r_end = SYNC >= 3 ? t_begin + tiles_per_wg : t_end;
-    for (uint32_t r0 = t_begin; r0 < r_end; r0 += kRound) {  // workgroup-uniform
+    DynQueue dq;
+    if (DYN && threadIdx.x == 0) dq.init(a, TPW);
+    uint32_t r0 = t_begin;
+    for (;;) {  // rounds, workgroup-uniform
+        // slot i of this round: wave w streams tile ub[i] + w when it is below ue[i]
+        uint32_t ub[TPW], ue[TPW];
+        if (DYN) {
+            if (threadIdx.x == 0) dq.claim_round<TPW>(sm.claim);
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                ub[i] = uniform(sm.claim[i][0]);
+                ue[i] = uniform(sm.claim[i][1]);
+            }
+            __syncthreads();  // the claim slots are rewritten next round
+            if (ub[0] >= ue[0]) break;  // claims go in order: slot 0 empty = every region exhausted
+        } else {
+            if (r0 >= r_end) break;
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                ub[i] = r0 + (uint32_t)i * kWaves6;
+                ue[i] = t_end;
+            }
+            r0 += kRound;
+        }
         u32x4 rec[TPW];
         uint32_t verd[TPW], alo[TPW], ahi[TPW];
         uint64_t wbm[TPW];
@@ -906,13 +1005,13 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         // ================= read phase =================
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const uint32_t t = r0 + (uint32_t)i * kWaves6 + wave;
+            const uint32_t t = ub[i] + wave;
             wbm[i] = 0ull;
             rec[i] = u32x4{0u, 0u, 0u, 0u};
             verd[i] = 0u;
             alo[i] = 0u;
             ahi[i] = 0u;
-            if (t >= t_end) continue;  // wave-uniform
+            if (t >= ue[i]) continue;  // wave-uniform
             asm volatile("" : "+v"(lane));
             uint8_t* rows = s_hdr[wave][i];
             const uint32_t q = lane >> 4, k = lane & 15u;
@@ -923,10 +1022,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
             if (PF) {
                 dsc = dnext;
-                const uint32_t tn = i + 1 < TPW ? t + (uint32_t)kWaves6 : r0 + kRound + wave;  // next tile
+                const uint32_t tn = i + 1 < TPW ? t + (uint32_t)kWaves6 : r0 + wave;  // next tile (r0: next round)
                 const uint32_t fn = tn * kTile + lane;
                 dnext = u32x4{0u, 0u, 0u, 0u};
                 if (tn < t_end && fn < a.n) dnext = *(const u32x4*)(a.descs + fn);
+            } else if (DLDS && a.desc_in_lds) {
+                if (in_n) dsc = sm.desc[fi];  // n <= 64: fi < 64
             } else if (in_n) {
                 dsc = *(const u32x4*)(a.descs + fi);
             }
@@ -969,6 +1070,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             ahi[i] = dsc.y;
             if (SYNC == 2) round_bytes += wave_sum_u32(in_n ? min(len, 65536u) : 0u);
 
+            if (TRACE && threadIdx.x == 0 && i == 0) a.trace[0] = wall_clock64();  // descriptors parsed
             // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
             if (__ballot(nit != 0u) != 0ull) {
                 __builtin_amdgcn_wave_barrier();
@@ -984,7 +1086,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     for (int r = 0; r < 8; ++r) {
                         const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
                         const bool in = ro < fm.lim;
-                        x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? meta6_a16(fm) + ro : 0ull)));
+                        x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
+                        if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
                     }
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
@@ -1002,7 +1105,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     for (int r = 0; r < 4; ++r) {
                         const FrameMeta6& fm = meta[(uint32_t)r * 16u + (lane >> 2)];
                         const bool in = ro < fm.lim;
-                        x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? meta6_a16(fm) + ro : 0ull)));
+                        x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
+                        if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
                     }
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -1039,7 +1143,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     for (int r = 0; r < 8; ++r) {
                         const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
                         const bool in = ro < fm.lim;
-                        x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + (in ? meta6_a16(fm) + ro : 0ull)));
+                        x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
+                        if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
                     }
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
@@ -1099,6 +1204,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 
             // ---- 3. header phase (lane = frame); the window stays patched in LDS ---------------------
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (TRACE && threadIdx.x == 0 && i == 0) a.trace[1] = wall_clock64();  // frames streamed
             __builtin_amdgcn_wave_barrier();
             const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
             const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
@@ -1114,6 +1220,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             __builtin_amdgcn_wave_barrier();  // meta/sums are rewritten by the next tile
         }
 
+        if (TRACE && threadIdx.x == 0) a.trace[2] = wall_clock64();  // header phase done
         // ================= write phase: every wave of the workgroup has finished reading =================
         if (SYNC == 1) __syncthreads();
         if (SYNC >= 3 && gbar) {  // every workgroup of the chip has finished reading this round
@@ -1139,12 +1246,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         }
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const uint32_t t = r0 + (uint32_t)i * kWaves6 + wave;
+            const uint32_t t = ub[i] + wave;
             if (NOWR) {  // keep the read phase alive without storing: fold the records into a counter
-                if (t < t_end) cnt.rxb += rec[i].x ^ rec[i].w ^ (uint32_t)wbm[i];
+                if (t < ue[i]) cnt.rxb += rec[i].x ^ rec[i].w ^ (uint32_t)wbm[i];
                 continue;
             }
-            if (t >= t_end) continue;
+            if (t >= ue[i]) continue;
             const uint8_t* rows = s_hdr[wave][i];
             if (wbm[i]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
 #pragma unroll
@@ -1186,7 +1293,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             __syncthreads();
         }
     }
+    if (DYN && threadIdx.x == 0) dq.leave();
+    if (TRACE && threadIdx.x == 0) a.trace[3] = wall_clock64();  // write phase issued
     store_partials<kWaves6>(a, cnt, s_cnt, wave, lane);
+    if (TRACE && threadIdx.x == 0) a.trace[4] = wall_clock64();  // counters added
     if (WGT && threadIdx.x == 0 && a.partials) {
         a.partials[8192 + 2 * blockIdx.x] = wgt_start;
         a.partials[8192 + 2 * blockIdx.x + 1] = wall_clock64();
@@ -1195,16 +1305,18 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 
 // One 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg tiles (echo6_geometry).
 // SUBT: tiles of a.tile_live frames (small batches, one workgroup).
+// DYN: the dynamic round schedule (DynQueue) instead of the static shares.
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
-          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false>
+          bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
+          bool DYN = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT>(a, t_begin, t_end, tiles_per_wg,
-                                                                                   sm);
+    echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN>(a, t_begin, t_end,
+                                                                                        tiles_per_wg, sm);
 }
 
 

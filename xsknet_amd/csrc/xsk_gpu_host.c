@@ -182,6 +182,7 @@ int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t ume
 }
 
 uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* c) { return c ? c->max_batch : 0u; }
+xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
 
 /* Uniform stride S (>= 64, multiple of 16) when addr[i] = addr[0] + i*S for the whole chunk. */
 static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
@@ -243,8 +244,9 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
     if (zerocopy(c)) { /* descriptors in, verdicts and counters out: mapped host memory */
         memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
         memset(&c->h_stats[ci], 0, sizeof c->h_stats[ci]);
+        const uint32_t tile = n <= XSK_GPU_LOWLAT_MAX ? xsk_gpu__small_tile(descs + i0, n) : 0u;
         rc = xsk_gpu__echo_dev_opts_hoststats(c->d_umem, c->umem_size, c->m_descs + i0, n, c->opts, c->m_verd + i0,
-                                   want_recs ? c->d_recs + i0 : NULL, c->m_stats + ci, c->d_ws[s], st);
+                                              want_recs ? c->d_recs + i0 : NULL, c->m_stats + ci, c->d_ws[s], st, tile);
         if (rc) goto out;
         TRY(hipEventRecord(c->done[ci], st));
         return 0;
@@ -279,8 +281,7 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
     if (!c || (!descs && n)) return -EINVAL;
     if (n == 0) return 0;
     if (n > c->max_batch) return -EINVAL;
-    TRY(hipSetDevice(c->device));
-    if (c->ll && n <= XSK_GPU_LOWLAT_MAX) { /* the doorbell: no launch, no synchronisation */
+    if (c->ll && n <= XSK_GPU_LOWLAT_MAX) { /* the doorbell: no launch, no synchronisation, no HIP call */
         memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
         rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL);
         if (rc) return rc;
@@ -295,6 +296,7 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
         }
         return 0;
     }
+    TRY(hipSetDevice(c->device));
     if (c->ll) xsk_gpu__lowlat_stop(c->ll); /* a large batch: the launch path (its streams never wait on it) */
     const uint32_t chunk = c->mode == XSK_GPU_MODE_STAGED ? CHUNK_FRAMES : n;
     const uint32_t nchunks = (n + chunk - 1) / chunk;

@@ -18,11 +18,28 @@ XSK_GPU__HIDDEN int xsk_gpu__pack_headers_dev(const void* d_umem, const struct x
                                               const uint8_t* d_verdicts, uint32_t n, uint8_t* d_pack, uint32_t wire,
                                               void* stream);
 
-/* xsk_echo.hip: xsk_gpu_echo_dev_opts for counters in mapped host memory (no device atomics) */
+/* xsk_echo.hip: xsk_gpu_echo_dev_opts for counters in mapped host memory (no device atomics): d_stats
+ * must be a slot zeroed for this call (a one-workgroup launch stores the counters without reading it).
+ * tile: frames per wave of a small batch (xsk_gpu__small_tile), 0 = ceil(n / 16). */
 XSK_GPU__HIDDEN int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size,
                                                      const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t opts,
                                                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
-                                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream);
+                                                     struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream,
+                                                     uint32_t tile);
+
+/* Frames per wave for a small batch (n <= XSK_GPU_LOWLAT_MAX) whose frames are read across PCIe: about
+ * 8 KiB of frame bytes per wave, 1..16 waves (a 64-frame batch of minimum-size frames is one wave: its
+ * few PCIe reads are better in one wave's hands than queued behind sixteen; 1500-B frames spread over
+ * every wave).  A multiple of 4 in [4, 64]. */
+static inline uint32_t xsk_gpu__small_tile(const struct xsk_gpu_desc* descs, uint32_t n) {
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < n; i++) bytes += descs[i].len < 4096u ? descs[i].len : 4096u;
+    uint64_t waves = (bytes + 8191u) / 8192u;
+    waves = waves < 1 ? 1 : (waves > 16 ? 16 : waves);
+    uint32_t t = (uint32_t)((n + waves - 1) / waves);
+    t = (t + 3u) & ~3u;
+    return t < 4u ? 4u : (t > 64u ? 64u : t);
+}
 
 /* xsk_gpu_host.c: xsk_gpu_init over a UMEM the caller has already registered with the HIP runtime
  * (portable + mapped, e.g. the one registration of a multi-GPU object): the context neither registers
@@ -37,16 +54,25 @@ XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
 struct xsk_gpu__bell {
     /* host -> device: ONE 64-bit word, so a poll is one PCIe read:
      *   bits 0-31 seq (bumped by one per posted batch), 32-47 n (<= XSK_GPU_LOWLAT_MAX),
-     *   bit 48 write records, bit 63 stop (the persistent kernel exits at its next poll) */
+     *   bit 48 write records, bits 49-55 frames per wave / 4 (0: ceil(n / 16)),
+ *   bit 63 stop (the persistent kernel exits at its next poll) */
     volatile uint64_t cmd;
     uint32_t pad0[30];
     /* device -> host */
     volatile uint32_t done;  /* seq of the last completed batch                               */
     volatile uint32_t alive; /* 1 while the persistent kernel runs                            */
-    uint32_t pad1[30];
+    /* diagnostics of the last batch, 100-MHz ticks: phase durations (one doorbell read, acquire +
+     * barrier, the transform body, release + barrier), then wave 0's clock at the body's phase
+     * boundaries relative to the body's start (descriptors, frames streamed, header phase, writes
+     * issued, counters added) */
+    volatile uint64_t trace[4];
+    volatile uint64_t body[6];
+    volatile uint64_t clk[2];  /* shader-clock (s_memtime) ticks and wall ticks over the last body */
+    uint32_t pad1[6];
 };
 #define XSK_GPU__BELL_N(n) ((uint64_t)(n) << 32)
 #define XSK_GPU__BELL_RECS (1ull << 48)
+#define XSK_GPU__BELL_TILE(q) ((uint64_t)((q) & 0x7Fu) << 49)
 #define XSK_GPU__BELL_STOP (1ull << 63)
 
 typedef struct xsk_gpu__lowlat xsk_gpu__lowlat;
@@ -63,6 +89,12 @@ XSK_GPU__HIDDEN struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN struct xsk_gpu_stats* xsk_gpu__lowlat_stats(xsk_gpu__lowlat* ll);
+/* Diagnostics (tools/hostlat.py): the phase durations of a LOWLAT context's last doorbell batch, in
+ * nanoseconds: out[0..3] the trace[] phases, out[4..8] body[0..4] relative to the body's start; out[9]
+ * the shader clock over the last body, in MHz; out[10..11] the host's time from entry to the doorbell
+ * store and from there to seeing the completion. */
+int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[12]);
+XSK_GPU__HIDDEN xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* ctx);
 
 #ifdef __cplusplus
 }

@@ -65,19 +65,39 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
     __shared__ uint32_t s_cmd[3];  // work?, n, recs
     xsk_gpu__bell* bell = L.bell;
     uint32_t served = 0;
-    if (threadIdx.x == 0) {
-        served = ld_sys(&bell->done);  // a previous instance's last batch (stream order: it has exited)
+    uint64_t t_seen = 0, t_poll = 0;  // wave 0: diagnostics
+    if (threadIdx.x < 64) {  // wave 0 polls; every lane keeps the same `served`
+        served = uniform(ld_sys(&bell->done));  // a previous instance's last batch (stream order: it has exited)
         st_sys(&bell->alive, 1u);
     }
+    const uint32_t lane = threadIdx.x & 63u;
     while (true) {
-        if (threadIdx.x == 0) {
-            uint32_t work = 0, n = 0, recs = 0;
-            uint64_t t0 = wall_clock64();
+        if (threadIdx.x < 64) {
+            // wave 0 polls: every read brings the command word AND the first 64 descriptor slots, so a
+            // batch of <= 64 frames needs no second round trip for its descriptors; the host tags each
+            // slot's `options` with the batch's sequence number, and a slot seen with an older tag (its
+            // write not yet visible) makes the wave poll again
+            uint32_t work = 0, n = 0, recs = 0, tq = 0, dl = 0;
+            uint64_t t0 = wall_clock64(), tr = 0, it = 0;
+            const uint64_t* dp = (const uint64_t*)(L.descs + lane);
+            const uint64_t t_loop = t0;
             while (true) {
-                const uint64_t c = ld_sys64(&bell->cmd);  // one PCIe read per poll
+                ++it;
+                const uint64_t cv = ld_sys64(&bell->cmd);
+                const uint64_t d0 = __hip_atomic_load((uint64_t*)dp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t d1 = __hip_atomic_load((uint64_t*)dp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t c = ((uint64_t)uniform((uint32_t)(cv >> 32)) << 32) | uniform((uint32_t)cv);
+                tr = (wall_clock64() - t_loop) / it;  // mean poll period so far
                 if ((uint32_t)c != served) {
-                    n = (uint32_t)(c >> 32) & 0xFFFFu;
+                    const uint32_t nn = (uint32_t)(c >> 32) & 0xFFFFu;
+                    if (nn <= (uint32_t)kTile) {
+                        if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) continue;  // not yet
+                        sm.desc[lane] = u32x4{(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)};
+                        dl = 1;
+                    }
+                    n = nn;
                     recs = (uint32_t)(c >> 48) & 1u;
+                    tq = (uint32_t)(c >> 49) & 0x7Fu;
                     served = (uint32_t)c;
                     work = 1;
                     break;
@@ -88,7 +108,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                     __hip_atomic_store((uint32_t*)&bell->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
                     const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
                                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    if ((uint32_t)c2 == served || (c2 & XSK_GPU__BELL_STOP)) break;
+                    if (uniform((uint32_t)c2) == served || (uniform((uint32_t)(c2 >> 32)) & 0x80000000u)) break;
                     st_sys(&bell->alive, 1u);
                     t0 = wall_clock64();
                     continue;
@@ -96,14 +116,22 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                 __builtin_amdgcn_s_sleep(2);
             }
             if (n > (uint32_t)XSK_GPU_LOWLAT_MAX) n = XSK_GPU_LOWLAT_MAX;  // the host never posts more
-            s_cmd[0] = work;
-            s_cmd[1] = n;
-            s_cmd[2] = recs;
+            if (lane == 0) {
+                s_cmd[0] = work;
+                s_cmd[1] = n;
+                s_cmd[2] = recs | (tq << 8) | (dl << 16);
+            }
+            t_seen = wall_clock64();
+            t_poll = tr;
         }
         __syncthreads();
-        const uint32_t work = s_cmd[0], n = s_cmd[1], recs = s_cmd[2];
+        const uint32_t work = s_cmd[0], n = s_cmd[1], recs = s_cmd[2] & 1u, tq = (s_cmd[2] >> 8) & 0xFFu;
+        const uint32_t dl = s_cmd[2] >> 16;
         if (!work) break;  // workgroup-uniform
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: fresh descriptors and frames
+        __syncthreads();
+        const uint64_t t_body = wall_clock64();
+        const uint64_t c_body = __builtin_amdgcn_s_memtime();
         EchoArgs a;
         a.umem = L.umem;
         a.umem_size = L.umem_size;
@@ -115,18 +143,32 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         a.opts = L.opts;
         a.stats_direct = (unsigned long long*)&L.stats->rx_packets;  // zeroed by the host before posting
         a.stats_plain = 1;                                            // the only writer
+        a.trace = (unsigned long long*)bell->body;
+        a.desc_in_lds = dl;
         // spread the batch over all 16 waves: tiles of ceil(n / 16) frames (a multiple of 4: one 16-lane
         // row per frame and step), so a 64-frame batch is 16 tiles of 4 frames, each wave one step
-        uint32_t tl = ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
+        uint32_t tl = tq ? 4u * tq : ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
         tl = tl < 4u ? 4u : (tl > (uint32_t)kTile ? (uint32_t)kTile : tl);
         a.tile_live = tl;
         const uint32_t ntiles = (n + tl - 1) / tl;
         if (ntiles)
             echo6_body<kShip6U, kLLTPW, kLLSync, kShip6Stream, false, false, WIRE, false, false, !WIRE && kShip6Mid,
-                       kShip6D2 && !WIRE, kShip6Skm && !WIRE, true>(a, 0u, ntiles, ntiles, sm);
+                       kShip6D2 && !WIRE, kShip6Skm && !WIRE, true, false, true, true>(a, 0u, ntiles, ntiles, sm);
+        const uint64_t t_rel = wall_clock64();
+        const uint64_t c_rel = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's stores are performed
-        __syncthreads();
-        if (threadIdx.x == 0) st_sys(&bell->done, served);
+        __syncthreads();  // (also: sm.desc is rewritten by the next poll only after every wave is done)
+        if (threadIdx.x == 0) {
+            const uint64_t t_end = wall_clock64();
+            st_sys(&bell->done, served);  // completion first: the diagnostics below are not waited for
+            bell->trace[0] = t_poll;
+            bell->trace[1] = t_body - t_seen;
+            bell->trace[2] = t_rel - t_body;
+            bell->trace[3] = t_end - t_rel;
+            bell->body[5] = t_body;
+            bell->clk[0] = c_rel - c_body;
+            bell->clk[1] = t_rel - t_body;
+        }
     }
 }
 
@@ -143,10 +185,13 @@ struct xsk_gpu__lowlat {
     struct xsk_gpu_rec* h_recs;
     struct xsk_gpu_stats* h_stats;
     int launched;  // a kernel instance was launched and may still run
-    uint32_t seq;  // last posted batch
+    uint32_t seq;     // last posted batch
+    uint32_t tile_q;  // frames per wave / 4 (0: ceil(n / 16)); XSK_GPU_LOWLAT_TILE (diagnostics)
+    uint64_t host_ns[2];  // last batch on the host: entry -> doorbell posted, posted -> completion seen
 };
 
 static int ll_launch(xsk_gpu__lowlat* ll) {
+    HIP_TRY(hipSetDevice(ll->device));
     __atomic_store_n(&ll->h_bell->cmd, (uint64_t)ll->seq, __ATOMIC_SEQ_CST);  // clears a stop request
     if (ll->args.opts)
         hipLaunchKernelGGL(lowlat_kernel<true>, dim3(1), dim3(kThreads6), 0, ll->stream, ll->args);
@@ -193,7 +238,11 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     xsk_gpu__lowlat* ll = (xsk_gpu__lowlat*)calloc(1, sizeof *ll);
     if (!ll) return -ENOMEM;
     int rc = 0;
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;  // fine-grained: polled across PCIe
+    // the doorbell is fine-grained (polled across PCIe); the data buffers are mapped like the UMEM itself:
+    // the kernel's system-scope acquire / release fences order them (selectable for measurements)
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    const char* dfe = getenv("XSK_GPU_LOWLAT_FINE");
+    const unsigned dfl = (dfe && dfe[0] == '1') ? fl : (unsigned)hipHostMallocMapped;
 #define LL_TRY(expr)                         \
     do {                                     \
         const hipError_t e_ = (expr);        \
@@ -210,10 +259,10 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     LL_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     LL_TRY(hipStreamCreateWithPriority(&ll->stream, hipStreamNonBlocking, hi));
     LL_TRY(hipHostMalloc((void**)&ll->h_bell, sizeof(xsk_gpu__bell), fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_desc), fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_stats, sizeof(struct xsk_gpu_stats), fl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_desc), dfl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, dfl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), dfl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_stats, sizeof(struct xsk_gpu_stats), dfl));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
     LowlatArgs& A = ll->args;
     LL_TRY(hipHostGetDevicePointer((void**)&A.bell, ll->h_bell, 0));
@@ -225,6 +274,10 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     A.umem = (uint8_t*)d_umem;
     A.umem_size = umem_size;
     A.opts = opts;
+    if (const char* e = getenv("XSK_GPU_LOWLAT_TILE")) {  // tuning: frames per wave (multiple of 4, <= 64)
+        const long t = strtol(e, nullptr, 10);
+        if (t >= 4 && t <= 64 && (t & 3) == 0) ll->tile_q = (uint32_t)(t / 4);
+    }
     *out = ll;
     return 0;  // the kernel starts with the first batch
 }
@@ -240,6 +293,7 @@ int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts) {
 int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
     if (!ll || n > XSK_GPU_LOWLAT_MAX) return -EINVAL;
     xsk_gpu__bell* b = ll->h_bell;
+    const double h_enter = now_s();
     int fresh = 0;  // a kernel launched by this call: it reads `done` at start and serves the new seq
     if (!ll->launched || !__atomic_load_n(&b->alive, __ATOMIC_SEQ_CST)) {
         // gone (idle exit) or never started: launch; stream order puts it behind an exiting instance
@@ -248,25 +302,30 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
         fresh = 1;
     }
     memset(ll->h_stats, 0, sizeof *ll->h_stats);
+    const uint32_t tq = ll->tile_q ? ll->tile_q : xsk_gpu__small_tile(ll->h_descs, n) / 4u;  // frames per wave / 4
     const uint32_t seq = ll->seq + 1u;
+    // tag the slots the polling wave reads with the doorbell (the transform never reads `options`)
+    for (uint32_t i = 0; i < (n < 64u ? n : 64u); i++) ll->h_descs[i].options = seq;
     ll->seq = seq;
     // descriptors and zeroed counters are written before this one store
-    __atomic_store_n(&b->cmd, (uint64_t)seq | XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull),
+    __atomic_store_n(&b->cmd, (uint64_t)seq | XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) |
+                                  XSK_GPU__BELL_TILE(tq),
                      __ATOMIC_SEQ_CST);
     if (!fresh && !__atomic_load_n(&b->alive, __ATOMIC_SEQ_CST)) {
         // the kernel was leaving (Dekker: it re-reads seq after clearing alive, or this launch serves it)
         const int rc = ll_launch(ll);
         if (rc) return rc;
     }
+    const double h_post = now_s();
     // spin on completion; past 200 us check the kernel is still there, past 2 s give up
-    double t0 = 0.0, tq = 0.0;
+    double t0 = 0.0, t_query = 0.0;
     for (uint32_t spin = 0;; ++spin) {
         if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) break;
         if ((spin & 1023u) == 1023u) {
             const double t = now_s();
-            if (t0 == 0.0) t0 = tq = t;
-            if (t - tq > 2e-4) {
-                tq = t;
+            if (t0 == 0.0) t0 = t_query = t;
+            if (t - t_query > 2e-4) {
+                t_query = t;
                 if (hipStreamQuery(ll->stream) == hipSuccess && __atomic_load_n(&b->done, __ATOMIC_ACQUIRE) != seq) {
                     const int rc = ll_launch(ll);  // exited without serving the batch: serve it now
                     if (rc) return rc;
@@ -277,6 +336,9 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
         __builtin_ia32_pause();
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    const double h_done = now_s();
+    ll->host_ns[0] = (uint64_t)((h_post - h_enter) * 1e9);
+    ll->host_ns[1] = (uint64_t)((h_done - h_post) * 1e9);
     return 0;
 }
 
@@ -284,6 +346,19 @@ struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll) { return ll->h_d
 uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll) { return ll->h_verd; }
 struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll) { return ll->h_recs; }
 struct xsk_gpu_stats* xsk_gpu__lowlat_stats(xsk_gpu__lowlat* ll) { return ll->h_stats; }
+
+int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[12]) {
+    xsk_gpu__lowlat* ll = xsk_gpu__ctx_lowlat(ctx);
+    for (int i = 0; i < 12; ++i) out_ns[i] = 0;
+    if (!ll) return -EINVAL;
+    const volatile xsk_gpu__bell* b = ll->h_bell;
+    for (int i = 0; i < 4; ++i) out_ns[i] = b->trace[i] * 10u;
+    for (int i = 0; i < 5; ++i) out_ns[4 + i] = b->body[i] > b->body[5] ? (b->body[i] - b->body[5]) * 10u : 0u;
+    out_ns[9] = b->clk[1] ? b->clk[0] * 100u / b->clk[1] : 0u;  // MHz
+    out_ns[10] = ll->host_ns[0];
+    out_ns[11] = ll->host_ns[1];
+    return 0;
+}
 
 void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll) { ll_free(ll); }
 
