@@ -428,7 +428,7 @@ def test_timing_hook():
     assert cnt == 3 and ms > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96, 99, 101])
 @pytest.mark.parametrize("grid", [0, 1, 7])
 @pytest.mark.parametrize("len_hi", [2048, 112, 48])
 def test_kernel_variants_parity(variant, grid, len_hi):
@@ -458,17 +458,17 @@ def test_kernel_variants_parity(variant, grid, len_hi):
     assert (d_verd.cpu().numpy() == v_ref).all()
     assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
     assert (d_umem.cpu().numpy() == ref).all()
-    if variant in (93, 95):  # the dynamic schedule leaves its queue counters zeroed for the next launch
+    if variant in (93, 95, 99, 101):  # dynamic schedules leave their queue counters zeroed for the next launch
         assert int(ws[768 << 10:(768 << 10) + 36].sum().item()) == 0
 
 
 def test_dynamic_schedule_full_size_and_reuse():
-    """The dynamic round schedule (tuning variants 93 / 95) over 1 M mixed frames, three launches on one
+    """The dynamic schedules (tuning variants 93 / 95: per-XCD rounds; 99: a tail pool) over 1 M mixed frames, three launches on one
     workspace: every frame exact each time (the counters reset themselves between launches)."""
     L = X.tune_lib()
     dev = _dev()
     n, stride = 1 << 20, 2048
-    for variant in (93, 95):
+    for variant in (93, 95, 99):
         d_umem = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
         d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
         X.synth_dev(d_umem, d_descs, n, 0, stride, 0x5EED9393, 0, 1, 0, 64, 1500)

@@ -96,7 +96,7 @@ def main():
                     if rep > 0:
                         times[(v, g)].extend(evs)
             torch.cuda.synchronize()
-        for wv in [v for v in variants if v in (79, 94)]:  # per-workgroup start/end wall clock (workspace tail)
+        for wv in [v for v in variants if v in (79, 94, 102)]:  # per-workgroup start/end wall clock (workspace tail)
             torch.cuda.synchronize()  # batch wv's launch reads is a request batch (every sweep re-arms)
             assert L.xsk_gpu__echo_variant(wv, 0, umems[0].data_ptr(), n * stride, descss[0].data_ptr(), n,
                                            verds[0].data_ptr(), recs.data_ptr(), ws.data_ptr(), sp) == 0

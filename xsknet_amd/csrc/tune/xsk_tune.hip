@@ -345,13 +345,13 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
     args.recs = d_recs;
     args.partials = (unsigned long long*)d_workspace;
     hipStream_t s = (hipStream_t)stream;
-    if (variant >= 60 && variant < 100) {  // round kernel: max_grid = workgroups (0: one per CU)
+    if (variant >= 60 && variant < 200) {  // round kernel: max_grid = workgroups (0: one per CU)
         int device = 0;
         HIP_TRY(hipGetDevice(&device));
         uint32_t g6 = 0, per = 0;
         echo6_geometry(n, max_grid ? max_grid : xsk_gpu__num_cu(device), &g6, &per);
         const dim3 gg(g6), bb(kThreads6);
-        if (variant >= 93 && variant <= 95) {  // queue counters at workspace + 768 KiB: zero, left zero
+        if ((variant >= 93 && variant <= 95) || (variant >= 99 && variant <= 102)) {  // queue counters at workspace + 768 KiB: zero, left zero
             if (!d_workspace) return -EINVAL;
             args.queue = (uint32_t*)((uint8_t*)d_workspace + (768u << 10));
         }
@@ -399,6 +399,12 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             // 97 / 98: the shipped kernel with 6 / 8 row-loads in flight per lane (a 1500-B frame in one batch)
             case 97: echo_kernel6<6, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 98: echo_kernel6<8, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 99-102: the shipped kernel + a tail pool of ntiles / TAIL tiles in 256-frame units (TAIL 8, 16, 4;
+            // 102 = TAIL 8 with WGT end-time probes)
+            case 99: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 8><<<gg, bb, 0, s>>>(args, per); break;
+            case 100: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 16><<<gg, bb, 0, s>>>(args, per); break;
+            case 101: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 4><<<gg, bb, 0, s>>>(args, per); break;
+            case 102: echo_kernel6<4, 2, 2, 2, false, true, false, false, false, true, true, true, false, false, 8><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;

@@ -1306,17 +1306,64 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // One 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg tiles (echo6_geometry).
 // SUBT: tiles of a.tile_live frames (small batches, one workgroup).
 // DYN: the dynamic round schedule (DynQueue) instead of the static shares.
+// TAIL (> 0): the last ntiles / TAIL tiles of the batch are not in the static shares but in a pool the
+// workgroups drain once their share is done, in units of 256 frames run as 16 sub-tiles of 16 frames (one
+// per wave) -- units a quarter of a tile's time, so the workgroups' end times even out (a.queue: one
+// counter, zero on entry, left zero).  The static shares cover the rest (tiles_per_wg is recomputed).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false>
+          bool DYN = false, int TAIL = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
     const uint32_t ntiles = (a.n + tl - 1) / tl;
-    const uint32_t t_begin = blockIdx.x * tiles_per_wg;
-    const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN>(a, t_begin, t_end,
-                                                                                        tiles_per_wg, sm);
+    if (TAIL == 0) {
+        const uint32_t t_begin = blockIdx.x * tiles_per_wg;
+        const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+        echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN>(a, t_begin, t_end,
+                                                                                            tiles_per_wg, sm);
+        return;
+    }
+    static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
+    const uint64_t wgt_start = WGT ? wall_clock64() : 0ull;
+    __shared__ uint32_t s_unit;
+    const uint32_t nt_tail = ntiles / (uint32_t)(TAIL > 0 ? TAIL : 1);
+    const uint32_t nt_s = ntiles - nt_tail;
+    const uint32_t per = (nt_s + gridDim.x - 1) / gridDim.x;
+    const uint32_t t_begin = min(nt_s, blockIdx.x * per);
+    const uint32_t t_end = min(nt_s, t_begin + per);
+    if (t_begin < t_end)
+        echo6_body<U, TPW, SYNC, STREAM, false, false, WIRE, NTS, NOWR, MID, D2, SKM>(a, t_begin, t_end, per, sm);
+    // the pool: frames [f0, n) in units of 256 (16 sub-tiles of 16 frames)
+    constexpr uint32_t kSub = 16, kUnit = kSub * kWaves6;
+    const uint32_t f0 = nt_s * kTile;
+    EchoArgs b = a;
+    b.descs = a.descs + f0;
+    b.verdicts = a.verdicts ? a.verdicts + f0 : nullptr;
+    b.recs = a.recs ? a.recs + f0 : nullptr;
+    b.n = a.n > f0 ? a.n - f0 : 0u;
+    b.tile_live = kSub;
+    const uint32_t units = (b.n + kUnit - 1) / kUnit, nsub = (b.n + kSub - 1) / kSub;
+    while (true) {
+        if (threadIdx.x == 0)
+            s_unit = __hip_atomic_fetch_add(a.queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t u = uniform(s_unit);
+        __syncthreads();  // s_unit is rewritten by the next claim
+        if (u >= units) break;
+        echo6_body<U, TPW, SYNC, STREAM, false, false, WIRE, NTS, NOWR, MID, D2, SKM, true>(
+            b, u * kWaves6, min(nsub, (u + 1) * kWaves6), kWaves6, sm);
+    }
+    if (threadIdx.x == 0) {  // the last workgroup out zeroes the counters for the next launch
+        if (__hip_atomic_fetch_add(a.queue + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u) {
+            __hip_atomic_store(a.queue, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.queue + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (WGT && a.partials) {
+            a.partials[8192 + 2 * blockIdx.x] = wgt_start;
+            a.partials[8192 + 2 * blockIdx.x + 1] = wall_clock64();
+        }
+    }
 }
 
 
