@@ -132,12 +132,46 @@ __global__ __launch_bounds__(256) void pack_headers_kernel(const uint8_t* umem, 
     for (uint32_t k = 0; k < w; ++k) q[k] = p[k];
 }
 
-// Re-arm TX_REPLY frames (lane per frame, byte granular: bench utility, not the hot path).
+// csum_replace2(csum, 0, 8) on the LE-loaded field: the inverse of the transform's (8 -> 0) patch
+__device__ __forceinline__ uint32_t rearm_csum(uint32_t c) {
+    uint32_t x = (~c) & 0xFFFFu;
+    x = (x + 0xFFFFu) & 0xFFFFu;
+    x += x < 0xFFFFu ? 1u : 0u;
+    x = (x + 8u) & 0xFFFFu;
+    x += x < 8u ? 1u : 0u;
+    return (~x) & 0xFFFFu;
+}
+
+// Re-arm TX_REPLY frames (lane per frame; bench utility, not the hot path).  A 16-B aligned frame (every
+// frame the bench generates) is re-armed as its whole 64-B sector -- four 16-B loads, the swaps as dword
+// shuffles, four 16-B stores: no partial-sector writes (the frame owns [addr, addr + max(len, 64)),
+// include/xsk_gpu.h); any other frame byte by byte.
 __global__ __launch_bounds__(256) void rearm_kernel(uint8_t* umem, const xsk_gpu_desc* descs, const uint8_t* verdicts,
                                                     uint32_t n) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= n || verdicts[i] != XSK_GPU_TX_REPLY) return;
     uint8_t* p = umem + descs[i].addr;
+    if ((descs[i].addr & 15u) == 0) {
+        u32x4* q = (u32x4*)p;
+        u32x4 a = q[0], b = q[1], c = q[2];
+        const u32x4 d = q[3];
+        // bytes 0-11: MACs swapped back (the same shuffle as the transform's, xsk_receive.c:148-151)
+        const uint32_t n0 = (a.y >> 16) | (a.z << 16), n1 = (a.z >> 16) | (a.x << 16), n2 = (a.x >> 16) | (a.y << 16);
+        a.x = n0;
+        a.y = n1;
+        a.z = n2;
+        // dwords 6, 7, 8 = bytes 24-35: IPv4 addresses swapped back (:153-155), type 0 -> 8 (byte 34)
+        const uint32_t h6 = b.z, h7 = b.w, h8 = c.x;
+        b.z = (h6 & 0xFFFFu) | (h7 & 0xFFFF0000u);
+        b.w = (h8 & 0xFFFFu) | (h6 & 0xFFFF0000u);
+        c.x = (h7 & 0xFFFFu) | (h8 & 0xFF000000u) | (8u << 16);
+        c.y = (c.y & 0xFFFF0000u) | rearm_csum(c.y & 0xFFFFu);  // bytes 36-37
+        q[0] = a;
+        q[1] = b;
+        q[2] = c;
+        q[3] = d;
+        return;
+    }
     uint8_t t[6];
     for (int k = 0; k < 6; ++k) t[k] = p[k];
     for (int k = 0; k < 6; ++k) p[k] = p[6 + k];
@@ -148,14 +182,7 @@ __global__ __launch_bounds__(256) void rearm_kernel(uint8_t* umem, const xsk_gpu
         p[30 + k] = x;
     }
     p[34] = 8;
-    // csum_replace2(csum, 0, 8) on the LE-loaded field
-    uint32_t c = (uint32_t)p[36] | ((uint32_t)p[37] << 8);
-    uint32_t x = (~c) & 0xFFFFu;
-    x = (x + 0xFFFFu) & 0xFFFFu;
-    x += x < 0xFFFFu ? 1u : 0u;
-    x = (x + 8u) & 0xFFFFu;
-    x += x < 8u ? 1u : 0u;
-    x = (~x) & 0xFFFFu;
+    const uint32_t x = rearm_csum((uint32_t)p[36] | ((uint32_t)p[37] << 8));
     p[36] = (uint8_t)x;
     p[37] = (uint8_t)(x >> 8);
 }

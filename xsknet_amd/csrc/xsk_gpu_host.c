@@ -285,14 +285,22 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
         memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
         rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL);
         if (rc) return rc;
-        const struct xsk_gpu_stats* hs = xsk_gpu__lowlat_stats(c->ll);
-        if (verdicts) memcpy(verdicts, xsk_gpu__lowlat_verdicts(c->ll), n);
+        const uint8_t* hv = xsk_gpu__lowlat_verdicts(c->ll);
+        if (verdicts) memcpy(verdicts, hv, n);
         if (recs) memcpy(recs, xsk_gpu__lowlat_recs(c->ll), (size_t)n * sizeof *recs);
-        if (stats) {
-            stats->rx_packets += hs->rx_packets;
-            stats->rx_bytes += hs->rx_bytes;
-            stats->tx_packets += hs->tx_packets;
-            stats->tx_bytes += hs->tx_bytes;
+        if (stats) { /* xsk_receive.c:171-172, 229, 233 -- what the kernel's counter phase would add */
+            uint64_t rxb = 0, txp = 0, txb = 0;
+            for (uint32_t i = 0; i < n; i++) {
+                rxb += descs[i].len;
+                if (hv[i] == XSK_GPU_TX_REPLY) {
+                    txp++;
+                    txb += descs[i].len;
+                }
+            }
+            stats->rx_packets += n;
+            stats->rx_bytes += rxb;
+            stats->tx_packets += txp;
+            stats->tx_bytes += txb;
         }
         return 0;
     }

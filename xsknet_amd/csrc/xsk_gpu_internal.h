@@ -84,11 +84,10 @@ XSK_GPU__HIDDEN void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts);
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
-/* Mapped host buffers the kernel reads / writes: descriptors, verdicts, records, counters. */
+/* Mapped host buffers the kernel reads / writes: descriptors, verdicts, records. */
 XSK_GPU__HIDDEN struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll);
-XSK_GPU__HIDDEN struct xsk_gpu_stats* xsk_gpu__lowlat_stats(xsk_gpu__lowlat* ll);
 /* Diagnostics (tools/hostlat.py): the phase durations of a LOWLAT context's last doorbell batch, in
  * nanoseconds: out[0..3] the trace[] phases, out[4..8] body[0..4] relative to the body's start; out[9]
  * the shader clock over the last body, in MHz; out[10..11] the host's time from entry to the doorbell

@@ -5,12 +5,13 @@
 // far more than the work, so this channel keeps ONE workgroup of the round kernel
 // resident: it polls a doorbell in fine-grained pinned host memory, runs the round kernel's body
 // (echo6_body, xsk_echo_device.h — the same code the launched kernel runs, bit for bit) over the posted
-// descriptors, writes verdicts, records and counters into mapped host memory, and publishes completion.
+// descriptors, writes verdicts and records into mapped host memory, and publishes completion (the host
+// adds the counters from the descriptors and verdicts it has anyway).
 // A batch is "write descriptors, bump the doorbell, spin on the completion word": no launch, no sync.
 //
 // Memory ordering (AMDGPU memory model, system scope): the host stores descriptors, then the doorbell
-// sequence number (x86 TSO keeps the order).  Thread 0 of the kernel reads the doorbell with a system-
-// scope acquire; after the workgroup barrier every wave issues a system-scope acquire fence, which
+// sequence number (x86 TSO keeps the order).  Wave 0 of the kernel polls the doorbell with relaxed
+// system-scope loads (two in flight); after the workgroup barrier every wave issues a system-scope acquire fence, which
 // invalidates the CU's L1 and the L2 lines of host memory, so recycled UMEM frames are never read stale.
 // After the body every wave issues a system-scope release fence (its stores to the UMEM, verdicts and
 // counters are performed and the L2 written back), the workgroup meets, and thread 0 stores the batch's
@@ -45,15 +46,11 @@ struct LowlatArgs {
     const xsk_gpu_desc* descs;
     uint8_t* verdicts;
     xsk_gpu_rec* recs;
-    xsk_gpu_stats* stats;
     uint32_t opts;
 };
 
 __device__ __forceinline__ uint32_t ld_sys(const volatile uint32_t* p) {
     return __hip_atomic_load((uint32_t*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t ld_sys64(const volatile uint64_t* p) {
-    return __hip_atomic_load((uint64_t*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void st_sys(volatile uint32_t* p, uint32_t v) {
     __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -79,19 +76,33 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             // write not yet visible) makes the wave poll again
             uint32_t work = 0, n = 0, recs = 0, tq = 0, dl = 0;
             uint64_t t0 = wall_clock64(), tr = 0, it = 0;
-            const uint64_t* dp = (const uint64_t*)(L.descs + lane);
             const uint64_t t_loop = t0;
-            while (true) {
+            // Two polls in flight, issued half a PCIe round trip apart (relaxed system-scope loads: no
+            // wait at issue; the acquire fence follows the barrier below), so the doorbell is sampled
+            // every ~0.6 us instead of every round trip.
+            // A descriptor slot is read with ONE 16-byte load (system-coherent: sc0 sc1), so the tag in its
+            // `options` word and its addr / len come from one snapshot of the host's cache line: a slot seen
+            // with the new tag has the new descriptor (the host writes the descriptor, then the tag, then
+            // the doorbell; x86 keeps that order).  Two separate 8-byte reads could tear.
+            const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)L.descs, (short)0, (int)(kTile * sizeof(xsk_gpu_desc)), kRsrcFlags);
+            constexpr int kSysCoherent = 1 | 16;  // cache policy SC0 | SC1
+            uint64_t cA, aA, bA, cB, aB, bB;
+            auto issue = [&](uint64_t& c, uint64_t& d0, uint64_t& d1) {
+                c = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(drs, (int)(lane * 16u), 0, kSysCoherent);
+                d0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
+                d1 = (uint64_t)d.z | ((uint64_t)d.w << 32);
+            };
+            // 0: keep polling, 1: a batch, 2: leave
+            auto examine = [&](uint64_t cv, uint64_t d0, uint64_t d1) -> int {
                 ++it;
-                const uint64_t cv = ld_sys64(&bell->cmd);
-                const uint64_t d0 = __hip_atomic_load((uint64_t*)dp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const uint64_t d1 = __hip_atomic_load((uint64_t*)dp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 const uint64_t c = ((uint64_t)uniform((uint32_t)(cv >> 32)) << 32) | uniform((uint32_t)cv);
-                tr = (wall_clock64() - t_loop) / it;  // mean poll period so far
+                tr = (wall_clock64() - t_loop) / it;  // mean sampling interval so far
                 if ((uint32_t)c != served) {
                     const uint32_t nn = (uint32_t)(c >> 32) & 0xFFFFu;
                     if (nn <= (uint32_t)kTile) {
-                        if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) continue;  // not yet
+                        if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) return 0;  // not yet
                         sm.desc[lane] = u32x4{(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)};
                         dl = 1;
                     }
@@ -100,20 +111,29 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                     tq = (uint32_t)(c >> 49) & 0x7Fu;
                     served = (uint32_t)c;
                     work = 1;
-                    break;
+                    return 1;
                 }
-                if (c & XSK_GPU__BELL_STOP) break;
+                if (c & XSK_GPU__BELL_STOP) return 2;
                 if (wall_clock64() - t0 > kIdleTicks) {
                     // leaving: clear `alive`, then look once more (the host posts, then reads `alive`)
                     __hip_atomic_store((uint32_t*)&bell->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
                     const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
                                                           __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (uniform((uint32_t)c2) == served || (uniform((uint32_t)(c2 >> 32)) & 0x80000000u)) break;
+                    if (uniform((uint32_t)c2) == served || (uniform((uint32_t)(c2 >> 32)) & 0x80000000u)) return 2;
                     st_sys(&bell->alive, 1u);
                     t0 = wall_clock64();
-                    continue;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                return 0;
+            };
+            issue(cA, aA, bA);
+            __builtin_amdgcn_s_sleep(22);  // ~0.6 us: half a round trip
+            while (true) {
+                issue(cB, aB, bB);
+                int r = examine(cA, aA, bA);  // waits for A only (B is still in flight)
+                if (r) break;
+                issue(cA, aA, bA);
+                r = examine(cB, aB, bB);
+                if (r) break;
             }
             if (n > (uint32_t)XSK_GPU_LOWLAT_MAX) n = XSK_GPU_LOWLAT_MAX;  // the host never posts more
             if (lane == 0) {
@@ -141,8 +161,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         a.recs = recs ? L.recs : nullptr;
         a.partials = nullptr;
         a.opts = L.opts;
-        a.stats_direct = (unsigned long long*)&L.stats->rx_packets;  // zeroed by the host before posting
-        a.stats_plain = 1;                                            // the only writer
+        a.stats_direct = nullptr;  // the host counts from the descriptors and verdicts: no counter phase
         a.trace = (unsigned long long*)bell->body;
         a.desc_in_lds = dl;
         // spread the batch over all 16 waves: tiles of ceil(n / 16) frames (a multiple of 4: one 16-lane
@@ -183,7 +202,6 @@ struct xsk_gpu__lowlat {
     struct xsk_gpu_desc* h_descs;
     uint8_t* h_verd;
     struct xsk_gpu_rec* h_recs;
-    struct xsk_gpu_stats* h_stats;
     int launched;  // a kernel instance was launched and may still run
     uint32_t seq;     // last posted batch
     uint32_t tile_q;  // frames per wave / 4 (0: ceil(n / 16)); XSK_GPU_LOWLAT_TILE (diagnostics)
@@ -228,7 +246,6 @@ static void ll_free(xsk_gpu__lowlat* ll) {
     if (ll->h_descs) (void)hipHostFree(ll->h_descs);
     if (ll->h_verd) (void)hipHostFree(ll->h_verd);
     if (ll->h_recs) (void)hipHostFree(ll->h_recs);
-    if (ll->h_stats) (void)hipHostFree(ll->h_stats);
     free(ll);
 }
 
@@ -262,14 +279,12 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_desc), dfl));
     LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, dfl));
     LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), dfl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_stats, sizeof(struct xsk_gpu_stats), dfl));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
     LowlatArgs& A = ll->args;
     LL_TRY(hipHostGetDevicePointer((void**)&A.bell, ll->h_bell, 0));
     LL_TRY(hipHostGetDevicePointer((void**)&A.descs, ll->h_descs, 0));
     LL_TRY(hipHostGetDevicePointer((void**)&A.verdicts, ll->h_verd, 0));
     LL_TRY(hipHostGetDevicePointer((void**)&A.recs, ll->h_recs, 0));
-    LL_TRY(hipHostGetDevicePointer((void**)&A.stats, ll->h_stats, 0));
 #undef LL_TRY
     A.umem = (uint8_t*)d_umem;
     A.umem_size = umem_size;
@@ -301,7 +316,6 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
         if (rc) return rc;
         fresh = 1;
     }
-    memset(ll->h_stats, 0, sizeof *ll->h_stats);
     const uint32_t tq = ll->tile_q ? ll->tile_q : xsk_gpu__small_tile(ll->h_descs, n) / 4u;  // frames per wave / 4
     const uint32_t seq = ll->seq + 1u;
     // tag the slots the polling wave reads with the doorbell (the transform never reads `options`)
@@ -345,7 +359,6 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
 struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll) { return ll->h_descs; }
 uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll) { return ll->h_verd; }
 struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll) { return ll->h_recs; }
-struct xsk_gpu_stats* xsk_gpu__lowlat_stats(xsk_gpu__lowlat* ll) { return ll->h_stats; }
 
 int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[12]) {
     xsk_gpu__lowlat* ll = xsk_gpu__ctx_lowlat(ctx);
