@@ -273,7 +273,11 @@ def main():
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus))  # nothing has touched a GPU in this process
+        # counting devices does not initialise the GPU on this image; nothing else here touches it
+        if not SHARE_GPU and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible "
+                             "(XSK_BENCH_SHARE_GPU=1 rehearses N ranks on one GPU)")
+        sys.exit(launch_ranks(args.gpus))
 
     import xsknet_amd as X
     from xsknet_amd import shard

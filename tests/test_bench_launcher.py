@@ -31,6 +31,7 @@ def test_launcher_spawns_n_ranks(monkeypatch):
         raise AssertionError("the launcher must not load the HIP library")
 
     monkeypatch.setattr(xsknet_amd, "lib", no_gpu)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5", "--config", "c5"])
     with pytest.raises(SystemExit) as e:
@@ -83,3 +84,14 @@ def test_launch_command_runs_ranks_with_gloo(tmp_path):
     r = subprocess.CompletedProcess(cmd, p.returncode, out, err)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "world 2 sum 3" in r.stdout
+
+
+def test_launcher_refuses_more_ranks_than_gpus(monkeypatch):
+    bench = _bench()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "SHARE_GPU", False)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "1 GPU(s) visible" in str(e.value)

@@ -4,13 +4,15 @@
  * per-descriptor process_packet() call replaced by one xsk_gpu_process() per batch.
  *
  *   echo_replay <umem.bin> <descs.bin> <out_umem.bin> <out_verdicts.bin> [batch] [zerocopy|staged|lowlat]
- *               [gpus=D0,D1,...] [reps=R]
+ *               [gpus=D0,D1,...] [reps=R] [flush=1] [huge=1]
  *
  * With gpus=..., the batches go through xsk_gpu_multi_process() over one context per listed device
  * (repeats allowed): descriptor i of a batch on context i mod G, counters summed on the host.
  * With reps=R (R >= 1), the replay is timed: R passes over the image, the UMEM restored from the input
  * between passes (untimed), and one more key=value pair, us_per_call (wall clock per batch call, the
  * first pass -- which starts the device side -- excluded), is printed; the outputs are those of pass 1.
+ * flush=1 evicts the restored UMEM from the CPU caches before each timed pass (frames a NIC delivered);
+ * huge=1 puts the UMEM on transparent huge pages.
  *
  * umem.bin: raw UMEM bytes (size multiple of 16).  descs.bin: packed struct xdp_desc records
  * (u64 addr, u32 len, u32 options).  Prints the stats_record counters the reference's stats
@@ -21,6 +23,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "../include/xsk_gpu.h"
@@ -51,6 +54,19 @@ static void* slurp(const char* path, size_t* size, size_t align) {
     return buf;
 }
 
+/* The UMEM on transparent huge pages (huge=1): 2-MiB aligned anonymous memory with MADV_HUGEPAGE, filled
+ * from the image.  AF_XDP accepts any page-aligned UMEM; the reference uses posix_memalign(getpagesize())
+ * (xsk_utils.c:135), i.e. 4-KiB pages, whose translations the GPU walks one page per frame. */
+static uint8_t* huge_copy(const uint8_t* src, size_t n) {
+    const size_t len = (n + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    void* p = mmap(NULL, len + (2u << 20), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return NULL;
+    uint8_t* a = (uint8_t*)(((uintptr_t)p + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1));
+    madvise(a, len, MADV_HUGEPAGE);
+    memcpy(a, src, n);
+    return a;
+}
+
 static int dump(const char* path, const void* p, size_t n) {
     FILE* f = fopen(path, "wb");
     if (!f) return -1;
@@ -72,7 +88,7 @@ int main(int argc, char** argv) {
     if (argc > 6 && strcmp(argv[6], "staged") == 0) mode = XSK_GPU_MODE_STAGED;
     if (argc > 6 && strcmp(argv[6], "lowlat") == 0) mode = XSK_GPU_MODE_LOWLAT;
     int devices[XSK_GPU_MULTI_MAX];
-    uint32_t ndev = 0, reps = 0;
+    uint32_t ndev = 0, reps = 0, flush = 0, huge = 0;
     for (int a = 7; a < argc; a++) {
         if (strncmp(argv[a], "gpus=", 5) == 0) {
             for (char* p = argv[a] + 5; *p && ndev < XSK_GPU_MULTI_MAX;) {
@@ -82,6 +98,10 @@ int main(int argc, char** argv) {
             }
         } else if (strncmp(argv[a], "reps=", 5) == 0) {
             reps = (uint32_t)strtoul(argv[a] + 5, NULL, 10);
+        } else if (strncmp(argv[a], "flush=", 6) == 0) {
+            flush = (uint32_t)strtoul(argv[a] + 6, NULL, 10);
+        } else if (strncmp(argv[a], "huge=", 5) == 0) {
+            huge = (uint32_t)strtoul(argv[a] + 5, NULL, 10);
         }
     }
     size_t umem_size = 0, desc_bytes = 0;
@@ -91,6 +111,15 @@ int main(int argc, char** argv) {
     if (!umem || !descs || batch == 0) {
         fprintf(stderr, "cannot read inputs\n");
         return 1;
+    }
+    if (huge) {
+        uint8_t* h = huge_copy(umem, umem_size);
+        if (!h) {
+            fprintf(stderr, "huge-page UMEM: mmap failed\n");
+            return 1;
+        }
+        free(umem);
+        umem = h; /* (never freed: the process ends) */
     }
     const uint32_t n = (uint32_t)(desc_bytes / sizeof *descs);
     uint8_t* verdicts = (uint8_t*)calloc(n ? n : 1, 1);
@@ -117,7 +146,13 @@ int main(int argc, char** argv) {
     double timed_s = 0.0;
     const uint32_t passes = reps ? reps : 1;
     for (uint32_t pass = 0; pass < passes; pass++) {
-        if (pass) memcpy(umem, pristine, umem_size); /* untimed: the frames are requests again */
+        if (pass) { /* untimed: the frames are requests again */
+            memcpy(umem, pristine, umem_size);
+            /* flush=1: out of the CPU caches, as frames a NIC wrote by DMA would be (a PCIe read of a line
+               dirty in a core's cache waits for the snoop) */
+            if (flush)
+                for (size_t o = 0; o < umem_size; o += 64) __builtin_ia32_clflush(umem + o);
+        }
         struct timespec t0, t1;
         clock_gettime(CLOCK_MONOTONIC, &t0);
         /* handle_receive_packets(): one RX peek of <= batch descriptors per iteration */
@@ -167,7 +202,7 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 12; i++) printf("%s%llu", i ? "," : "", (unsigned long long)tr[i]);
     }
     printf("\n");
-    free(umem);
+    if (!huge) free(umem);
     free(descs);
     free(verdicts);
     free(scratch);

@@ -25,7 +25,8 @@ import oracle  # noqa: E402  (frame generator only)
 
 
 def run_one(exe, p, flen, mode, batch, tile, args):
-    cmd = [exe, p("u"), p("d"), p("o"), p("v"), str(batch), mode, f"reps={args.reps}"]
+    cmd = [exe, p("u"), p("d"), p("o"), p("v"), str(batch), mode, f"reps={args.reps}"] + (["flush=1"] if args.flush else []) + \
+        (["huge=1"] if args.huge else [])
     if args.gpus:
         cmd.insert(7, f"gpus={args.gpus}")
     env = dict(os.environ, XSK_GPU_LOWLAT_TILE=tile) if tile else None
@@ -36,6 +37,7 @@ def run_one(exe, p, flen, mode, batch, tile, args):
     kv = dict(x.split("=") for x in r.stdout.split())
     us = float(kv["us_per_call"])
     rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto",
+           "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge),
            "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3), "calls": int(kv["calls"])}
     if "trace_ns" in kv:  # LOWLAT: the last batch's phases on the GPU
         t = [int(x) for x in kv["trace_ns"].split(",")]
@@ -54,6 +56,8 @@ def main():
     ap.add_argument("--batches", default="64,256,1024,4096")
     ap.add_argument("--gpus", default="")
     ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--flush", action="store_true", help="evict the UMEM from the CPU caches before each pass")
+    ap.add_argument("--huge", action="store_true", help="the UMEM on transparent huge pages (2 MiB)")
     ap.add_argument("--tiles", default="", help="LOWLAT frames per wave to sweep (XSK_GPU_LOWLAT_TILE), e.g. 4,16,64")
     args = ap.parse_args()
     exe = os.path.join(ROOT, "tools", "echo_replay")

@@ -60,6 +60,9 @@ template <bool WIRE>
 __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
     __shared__ Echo6Smem<kLLTPW, WIRE, kShip6Stream> sm;
     __shared__ uint32_t s_cmd[3];  // work?, n, recs
+    // the body's phase stamps land in the LDS and reach the host only after `done`: a store to host memory
+    // inside the body would put its PCIe acknowledgement in front of every later wait on a load
+    __shared__ unsigned long long s_trace[6];
     xsk_gpu__bell* bell = L.bell;
     uint32_t served = 0;
     uint64_t t_seen = 0, t_poll = 0;  // wave 0: diagnostics
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         a.partials = nullptr;
         a.opts = L.opts;
         a.stats_direct = nullptr;  // the host counts from the descriptors and verdicts: no counter phase
-        a.trace = (unsigned long long*)bell->body;
+        a.trace = s_trace;
         a.desc_in_lds = dl;
         // spread the batch over all 16 waves: tiles of ceil(n / 16) frames (a multiple of 4: one 16-lane
         // row per frame and step), so a 64-frame batch is 16 tiles of 4 frames, each wave one step
@@ -184,6 +187,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             bell->trace[1] = t_body - t_seen;
             bell->trace[2] = t_rel - t_body;
             bell->trace[3] = t_end - t_rel;
+            for (int k = 0; k < 5; ++k) bell->body[k] = s_trace[k];
             bell->body[5] = t_body;
             bell->clk[0] = c_rel - c_body;
             bell->clk[1] = t_rel - t_body;
