@@ -177,3 +177,27 @@ def test_multi_context_argument_checks():
     assert L.xsk_gpu_multi_init(C.byref(h), bad, 2, buf.ctypes.data, buf.nbytes, 64, 0) == -errno.ENODEV
     assert L.xsk_gpu_multi_process(None, None, 0, None, None, None) == -errno.EINVAL
     L.xsk_gpu_multi_fini(None)
+
+
+def test_lowlat_posts_near_idle_exit():
+    """Batches posted right around the resident kernel's 50-ms idle exit (the exit / relaunch race): every
+    batch is served exactly once and exactly right."""
+    _dev()
+    n, batch = 64 * 40, 64
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2323, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    work = umem.copy()
+    rng = np.random.default_rng(11)
+    tot = {k: 0 for k in COUNTERS}
+    with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_LOWLAT) as ctx:
+        for i in range(0, n, batch):
+            time.sleep(float(rng.uniform(0.046, 0.054)))
+            v, r, s = ctx.process(descs[i:i + batch])
+            assert (v == v_ref[i:i + batch]).all() and (r == r_ref[i:i + batch]).all(), i
+            for k in tot:
+                tot[k] += int(s[k])
+    for k in COUNTERS:
+        assert tot[k] == int(s_ref[k]), k
+    assert (work == ref).all()

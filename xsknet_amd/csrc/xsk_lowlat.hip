@@ -214,7 +214,10 @@ struct xsk_gpu__lowlat {
 
 static int ll_launch(xsk_gpu__lowlat* ll) {
     HIP_TRY(hipSetDevice(ll->device));
-    __atomic_store_n(&ll->h_bell->cmd, (uint64_t)ll->seq, __ATOMIC_SEQ_CST);  // clears a stop request
+    // clear a stop request, keeping a batch that may already be posted in the same word (the host is the
+    // word's only writer)
+    const uint64_t c = __atomic_load_n(&ll->h_bell->cmd, __ATOMIC_SEQ_CST);
+    if (c & XSK_GPU__BELL_STOP) __atomic_store_n(&ll->h_bell->cmd, c & ~XSK_GPU__BELL_STOP, __ATOMIC_SEQ_CST);
     if (ll->args.opts)
         hipLaunchKernelGGL(lowlat_kernel<true>, dim3(1), dim3(kThreads6), 0, ll->stream, ll->args);
     else
