@@ -46,6 +46,9 @@ def run_one(exe, p, flen, mode, batch, tile, args):
             "wave0_in_transform": {"descriptors": t[4] / 1e3, "streamed": t[5] / 1e3, "header_phase": t[6] / 1e3,
                                    "writes_issued": t[7] / 1e3, "counters": t[8] / 1e3},
             "shader_clock_mhz": t[9], "host_before_doorbell": t[10] / 1e3, "host_doorbell_to_done": t[11] / 1e3}
+        if len(t) >= 15 and t[12]:  # this kernel instance: doorbell reads per batch, stale descriptor reads
+            rec["polls_per_batch"] = round(t[13] / t[12], 2)
+            rec["stale_reads_per_batch"] = round(t[14] / t[12], 3)
     return rec
 
 

@@ -49,26 +49,35 @@ XSK_GPU__HIDDEN int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* um
 XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
 
 /* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context.  Shared memory
- * layout (mapped, fine-grained pinned host memory): host-written and device-written words live on
- * separate 128-byte lines. */
+ * layout (mapped, fine-grained pinned host memory): every word the host spins on or the kernel polls sits
+ * on a 64-byte line of its own. */
 struct xsk_gpu__bell {
     /* host -> device: ONE 64-bit word, so a poll is one PCIe read:
      *   bits 0-31 seq (bumped by one per posted batch), 32-47 n (<= XSK_GPU_LOWLAT_MAX),
      *   bit 48 write records, bits 49-55 frames per wave / 4 (0: ceil(n / 16)),
- *   bit 63 stop (the persistent kernel exits at its next poll) */
+     *   bit 63 stop (the persistent kernel exits at its next poll) */
     volatile uint64_t cmd;
-    uint32_t pad0[30];
+    uint32_t pad0[14];
+    /* the same word again in a line of its own: the kernel keeps two polls in flight, one per copy (two
+     * reads of ONE line do not overlap -- the second waits for the first) */
+    volatile uint64_t cmd_b;
+    uint32_t pad0b[14];
     /* device -> host */
-    volatile uint32_t done;  /* seq of the last completed batch                               */
-    volatile uint32_t alive; /* 1 while the persistent kernel runs                            */
-    /* diagnostics of the last batch, 100-MHz ticks: phase durations (one doorbell read, acquire +
-     * barrier, the transform body, release + barrier), then wave 0's clock at the body's phase
-     * boundaries relative to the body's start (descriptors, frames streamed, header phase, writes
-     * issued, counters added) */
-    volatile uint64_t trace[4];
-    volatile uint64_t body[6];
-    volatile uint64_t clk[2];  /* shader-clock (s_memtime) ticks and wall ticks over the last body */
-    uint32_t pad1[6];
+    volatile uint32_t done;  /* seq of the last completed batch */
+    volatile uint32_t alive; /* 1 while the persistent kernel runs */
+    uint32_t pad2[14];
+};
+
+/* Diagnostics of a LOWLAT kernel, in DEVICE memory (a store to host memory would put a PCIe
+ * acknowledgement in front of the next doorbell poll), read by xsk_gpu__lowlat_trace().  100-MHz ticks. */
+struct xsk_gpu__lldiag {
+    uint64_t trace[4];  /* last batch: mean doorbell sampling interval, acquire + barrier, body, release +
+                         * barrier + completion */
+    uint64_t body[6];   /* wave 0's clock at the body's phase boundaries (descriptors, frames streamed,
+                         * header phase, writes issued, counters), then the body's start */
+    uint64_t clk[2];    /* shader-clock (s_memtime) ticks and wall ticks over the last body */
+    uint64_t polls[3];  /* this kernel instance: batches served, doorbell reads examined, reads that saw a
+                         * new doorbell with descriptor slots not yet tagged */
 };
 #define XSK_GPU__BELL_N(n) ((uint64_t)(n) << 32)
 #define XSK_GPU__BELL_RECS (1ull << 48)
@@ -92,7 +101,7 @@ XSK_GPU__HIDDEN struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll);
  * nanoseconds: out[0..3] the trace[] phases, out[4..8] body[0..4] relative to the body's start; out[9]
  * the shader clock over the last body, in MHz; out[10..11] the host's time from entry to the doorbell
  * store and from there to seeing the completion. */
-int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[12]);
+int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[15]);
 XSK_GPU__HIDDEN xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* ctx);
 
 #ifdef __cplusplus

@@ -11,11 +11,13 @@
 //
 // Memory ordering (AMDGPU memory model, system scope): the host stores descriptors, then the doorbell
 // sequence number (x86 TSO keeps the order).  Wave 0 of the kernel polls the doorbell with relaxed
-// system-scope loads (two in flight); after the workgroup barrier every wave issues a system-scope acquire fence, which
-// invalidates the CU's L1 and the L2 lines of host memory, so recycled UMEM frames are never read stale.
-// After the body every wave issues a system-scope release fence (its stores to the UMEM, verdicts and
-// counters are performed and the L2 written back), the workgroup meets, and thread 0 stores the batch's
-// sequence number to `done` with a system-scope release.
+// system-scope loads (two in flight, one per copy of the word); on a new batch it issues ONE system-scope
+// acquire fence, which invalidates the CU's L1 (shared by the workgroup's waves) and the L2 lines of host
+// memory, so recycled UMEM frames are never read stale, then the workgroup meets.  After the body every
+// wave waits for its own stores' acknowledgements, the workgroup meets, and thread 0 issues ONE
+// system-scope release fence (the L2 write-back covers every wave's stores to the UMEM, verdicts and
+// records: one L2 per workgroup) and stores the batch's sequence number to `done`.  (A fence per wave
+// queued sixteen L2 write-backs in front of `done`.)
 //
 // Exit conditions every wave reaches: the host's stop word, or no batch for kIdleTicks (50 ms of the
 // 100-MHz wall clock) — so a process that dies without xsk_gpu_fini() never leaves the grid running.
@@ -39,11 +41,14 @@ constexpr uint64_t kIdleTicks = 5000000ull;  // 50 ms at 100 MHz (s_memrealtime)
 constexpr int kLLTPW = 1;                    // 16 tiles = 1024 frames per doorbell, one round
 constexpr int kLLSync = 0;                   // one round: write as soon as the wave has read
 
+constexpr int kPollCopies = 2;  // doorbell words (and first-64 descriptor blocks) polled in turn
+
 struct LowlatArgs {
     xsk_gpu__bell* bell;  // device alias of the mapped doorbell
+    xsk_gpu__lldiag* diag;  // device memory
     uint8_t* umem;
     uint64_t umem_size;
-    const xsk_gpu_desc* descs;
+    const xsk_gpu_desc* descs;  // XSK_GPU_LOWLAT_MAX slots, then a copy of the first 64 for the second poll
     uint8_t* verdicts;
     xsk_gpu_rec* recs;
     uint32_t opts;
@@ -60,17 +65,22 @@ template <bool WIRE>
 __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
     __shared__ Echo6Smem<kLLTPW, WIRE, kShip6Stream> sm;
     __shared__ uint32_t s_cmd[3];  // work?, n, recs
-    // the body's phase stamps land in the LDS and reach the host only after `done`: a store to host memory
-    // inside the body would put its PCIe acknowledgement in front of every later wait on a load
+    // the body's phase stamps land in the LDS and go to the device-memory diagnostics after `done`: a store
+    // to host memory would put its PCIe acknowledgement in front of every later wait on a load (the
+    // vector memory counter retires in order) -- and a volatile one waits for its own
     __shared__ unsigned long long s_trace[6];
     xsk_gpu__bell* bell = L.bell;
     uint32_t served = 0;
     uint64_t t_seen = 0, t_poll = 0;  // wave 0: diagnostics
+    uint64_t n_batches = 0, n_polls = 0, n_stale = 0;
     if (threadIdx.x < 64) {  // wave 0 polls; every lane keeps the same `served`
         served = uniform(ld_sys(&bell->done));  // a previous instance's last batch (stream order: it has exited)
         st_sys(&bell->alive, 1u);
     }
     const uint32_t lane = threadIdx.x & 63u;
+    // the two polls' registers live across the body: a batch is taken while the other poll is still in
+    // flight, and registers the compiler reused would first have to wait for it to land
+    uint64_t cA = 0, aA = 0, bA = 0, cB = 0, aB = 0, bB = 0;
     while (true) {
         if (threadIdx.x < 64) {
             // wave 0 polls: every read brings the command word AND the first 64 descriptor slots, so a
@@ -87,13 +97,18 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             // `options` word and its addr / len come from one snapshot of the host's cache line: a slot seen
             // with the new tag has the new descriptor (the host writes the descriptor, then the tag, then
             // the doorbell; x86 keeps that order).  Two separate 8-byte reads could tear.
+            // The two polls read different lines (`cmd` / `cmd_b`, slots 0-63 / their copy after the last
+            // slot): a read of a line that is already being read waits for the first to return, so polls
+            // of one line would sample the doorbell only once per round trip.
             const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)L.descs, (short)0, (int)(kTile * sizeof(xsk_gpu_desc)), kRsrcFlags);
+                (void*)L.descs, (short)0, (int)((XSK_GPU_LOWLAT_MAX + kTile) * sizeof(xsk_gpu_desc)), kRsrcFlags);
             constexpr int kSysCoherent = 1 | 16;  // cache policy SC0 | SC1
-            uint64_t cA, aA, bA, cB, aB, bB;
-            auto issue = [&](uint64_t& c, uint64_t& d0, uint64_t& d1) {
-                c = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(drs, (int)(lane * 16u), 0, kSysCoherent);
+            static_assert(kPollCopies == 2, "the loop below alternates two copies");
+            auto issue = [&](int copy, uint64_t& c, uint64_t& d0, uint64_t& d1) {
+                c = __hip_atomic_load((uint64_t*)(copy ? &bell->cmd_b : &bell->cmd), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+                const int dofs = (int)((copy ? XSK_GPU_LOWLAT_MAX : 0u) * sizeof(xsk_gpu_desc) + lane * 16u);
+                const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(drs, dofs, 0, kSysCoherent);
                 d0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
                 d1 = (uint64_t)d.z | ((uint64_t)d.w << 32);
             };
@@ -105,7 +120,10 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                 if ((uint32_t)c != served) {
                     const uint32_t nn = (uint32_t)(c >> 32) & 0xFFFFu;
                     if (nn <= (uint32_t)kTile) {
-                        if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) return 0;  // not yet
+                        if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) {
+                            ++n_stale;
+                            return 0;  // not yet
+                        }
                         sm.desc[lane] = u32x4{(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)};
                         dl = 1;
                     }
@@ -128,16 +146,22 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                 }
                 return 0;
             };
-            issue(cA, aA, bA);
+            issue(0, cA, aA, bA);
             __builtin_amdgcn_s_sleep(22);  // ~0.6 us: half a round trip
             while (true) {
-                issue(cB, aB, bB);
+                issue(1, cB, aB, bB);
                 int r = examine(cA, aA, bA);  // waits for A only (B is still in flight)
                 if (r) break;
-                issue(cA, aA, bA);
+                issue(0, cA, aA, bA);
                 r = examine(cB, aB, bB);
                 if (r) break;
             }
+            // ONE system-scope acquire for the workgroup (the barrier below orders the other waves after it):
+            // fresh descriptors and frames.  The doorbell read it follows has returned (it was examined);
+            // the other poll may still be in flight and is not waited for (the fence intrinsic would wait
+            // for every outstanding load first: up to half a round trip).  The invalidation travels the
+            // same path as every later load of the workgroup, so none of them can pass it.
+            if (work) asm volatile("buffer_inv sc0 sc1" ::: "memory");
             if (n > (uint32_t)XSK_GPU_LOWLAT_MAX) n = XSK_GPU_LOWLAT_MAX;  // the host never posts more
             if (lane == 0) {
                 s_cmd[0] = work;
@@ -146,13 +170,16 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             }
             t_seen = wall_clock64();
             t_poll = tr;
+            n_polls += it;
+            ++n_batches;
         }
-        __syncthreads();
+        // the command travels through the LDS only: an LDS-only barrier (__syncthreads() would first wait
+        // for wave 0's poll still in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         const uint32_t work = s_cmd[0], n = s_cmd[1], recs = s_cmd[2] & 1u, tq = (s_cmd[2] >> 8) & 0xFFu;
         const uint32_t dl = s_cmd[2] >> 16;
         if (!work) break;  // workgroup-uniform
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: fresh descriptors and frames
-        __syncthreads();
         const uint64_t t_body = wall_clock64();
         const uint64_t c_body = __builtin_amdgcn_s_memtime();
         EchoArgs a;
@@ -176,21 +203,30 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         if (ntiles)
             echo6_body<kShip6U, kLLTPW, kLLSync, kShip6Stream, false, false, WIRE, false, false, !WIRE && kShip6Mid,
                        kShip6D2 && !WIRE, kShip6Skm && !WIRE, true, false, true, true>(a, 0u, ntiles, ntiles, sm);
+        asm volatile("" ::"v"(cA), "v"(aA), "v"(bA), "v"(cB), "v"(aB), "v"(bB));
         const uint64_t t_rel = wall_clock64();
         const uint64_t c_rel = __builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's stores are performed
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have reached the L2 / fabric
         __syncthreads();  // (also: sm.desc is rewritten by the next poll only after every wave is done)
         if (threadIdx.x == 0) {
+            // system scope, once for the workgroup: write back the L2 lines of host memory the body wrote,
+            // wait for it, then publish completion (diagnostics after it: they are not waited for)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             const uint64_t t_end = wall_clock64();
-            st_sys(&bell->done, served);  // completion first: the diagnostics below are not waited for
-            bell->trace[0] = t_poll;
-            bell->trace[1] = t_body - t_seen;
-            bell->trace[2] = t_rel - t_body;
-            bell->trace[3] = t_end - t_rel;
-            for (int k = 0; k < 5; ++k) bell->body[k] = s_trace[k];
-            bell->body[5] = t_body;
-            bell->clk[0] = c_rel - c_body;
-            bell->clk[1] = t_rel - t_body;
+            __hip_atomic_store((uint32_t*)&bell->done, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // plain stores to device memory: no wait here, acknowledged long before the first poll returns
+            xsk_gpu__lldiag* dg = L.diag;
+            dg->trace[0] = t_poll;
+            dg->trace[1] = t_body - t_seen;
+            dg->trace[2] = t_rel - t_body;
+            dg->trace[3] = t_end - t_rel;
+            for (int k = 0; k < 5; ++k) dg->body[k] = s_trace[k];
+            dg->body[5] = t_body;
+            dg->clk[0] = c_rel - c_body;
+            dg->clk[1] = t_rel - t_body;
+            dg->polls[0] = n_batches;
+            dg->polls[1] = n_polls;
+            dg->polls[2] = n_stale;
         }
     }
 }
@@ -201,7 +237,7 @@ struct xsk_gpu__lowlat {
     int device;
     hipStream_t stream;
     xsk_gpu__bell* h_bell;
-    xsk_gpu__bell* d_bell;
+    xsk_gpu__lldiag* d_diag;
     LowlatArgs args;
     struct xsk_gpu_desc* h_descs;
     uint8_t* h_verd;
@@ -212,12 +248,17 @@ struct xsk_gpu__lowlat {
     uint64_t host_ns[2];  // last batch on the host: entry -> doorbell posted, posted -> completion seen
 };
 
+// the doorbell word and its copy (the host is their only writer)
+static void ll_post(xsk_gpu__bell* b, uint64_t c) {
+    __atomic_store_n(&b->cmd_b, c, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&b->cmd, c, __ATOMIC_SEQ_CST);
+}
+
 static int ll_launch(xsk_gpu__lowlat* ll) {
     HIP_TRY(hipSetDevice(ll->device));
-    // clear a stop request, keeping a batch that may already be posted in the same word (the host is the
-    // word's only writer)
+    // clear a stop request, keeping a batch that may already be posted in the same word
     const uint64_t c = __atomic_load_n(&ll->h_bell->cmd, __ATOMIC_SEQ_CST);
-    if (c & XSK_GPU__BELL_STOP) __atomic_store_n(&ll->h_bell->cmd, c & ~XSK_GPU__BELL_STOP, __ATOMIC_SEQ_CST);
+    if (c & XSK_GPU__BELL_STOP) ll_post(ll->h_bell, c & ~XSK_GPU__BELL_STOP);
     if (ll->args.opts)
         hipLaunchKernelGGL(lowlat_kernel<true>, dim3(1), dim3(kThreads6), 0, ll->stream, ll->args);
     else
@@ -239,7 +280,7 @@ void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll) {
     if (!ll) return;
     (void)hipSetDevice(ll->device);
     if (ll->launched) {
-        __atomic_store_n(&ll->h_bell->cmd, (uint64_t)ll->seq | XSK_GPU__BELL_STOP, __ATOMIC_SEQ_CST);
+        ll_post(ll->h_bell, (uint64_t)ll->seq | XSK_GPU__BELL_STOP);
         (void)hipStreamSynchronize(ll->stream);  // the kernel sees `stop` within one poll
         ll->launched = 0;
     }
@@ -250,6 +291,7 @@ static void ll_free(xsk_gpu__lowlat* ll) {
     xsk_gpu__lowlat_stop(ll);
     if (ll->stream) (void)hipStreamDestroy(ll->stream);
     if (ll->h_bell) (void)hipHostFree(ll->h_bell);
+    if (ll->d_diag) (void)hipFree(ll->d_diag);
     if (ll->h_descs) (void)hipHostFree(ll->h_descs);
     if (ll->h_verd) (void)hipHostFree(ll->h_verd);
     if (ll->h_recs) (void)hipHostFree(ll->h_recs);
@@ -283,12 +325,16 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     LL_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     LL_TRY(hipStreamCreateWithPriority(&ll->stream, hipStreamNonBlocking, hi));
     LL_TRY(hipHostMalloc((void**)&ll->h_bell, sizeof(xsk_gpu__bell), fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_desc), dfl));
+    // XSK_GPU_LOWLAT_MAX slots plus a copy of the first 64 (the second poll's)
+    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc), dfl));
     LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, dfl));
     LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), dfl));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
+    LL_TRY(hipMalloc((void**)&ll->d_diag, sizeof(xsk_gpu__lldiag)));
+    LL_TRY(hipMemset(ll->d_diag, 0, sizeof(xsk_gpu__lldiag)));
     LowlatArgs& A = ll->args;
     LL_TRY(hipHostGetDevicePointer((void**)&A.bell, ll->h_bell, 0));
+    A.diag = ll->d_diag;
     LL_TRY(hipHostGetDevicePointer((void**)&A.descs, ll->h_descs, 0));
     LL_TRY(hipHostGetDevicePointer((void**)&A.verdicts, ll->h_verd, 0));
     LL_TRY(hipHostGetDevicePointer((void**)&A.recs, ll->h_recs, 0));
@@ -325,13 +371,17 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
     }
     const uint32_t tq = ll->tile_q ? ll->tile_q : xsk_gpu__small_tile(ll->h_descs, n) / 4u;  // frames per wave / 4
     const uint32_t seq = ll->seq + 1u;
-    // tag the slots the polling wave reads with the doorbell (the transform never reads `options`)
-    for (uint32_t i = 0; i < (n < 64u ? n : 64u); i++) ll->h_descs[i].options = seq;
+    // tag the slots the polling wave reads with the doorbell (the transform never reads `options`), and
+    // copy them for the second poll
+    const uint32_t n64 = n < 64u ? n : 64u;
+    struct xsk_gpu_desc* shadow = ll->h_descs + XSK_GPU_LOWLAT_MAX;
+    for (uint32_t i = 0; i < n64; i++) {
+        ll->h_descs[i].options = seq;
+        shadow[i] = ll->h_descs[i];
+    }
     ll->seq = seq;
-    // descriptors and zeroed counters are written before this one store
-    __atomic_store_n(&b->cmd, (uint64_t)seq | XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) |
-                                  XSK_GPU__BELL_TILE(tq),
-                     __ATOMIC_SEQ_CST);
+    // descriptors are written before these stores
+    ll_post(b, (uint64_t)seq | XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) | XSK_GPU__BELL_TILE(tq));
     if (!fresh && !__atomic_load_n(&b->alive, __ATOMIC_SEQ_CST)) {
         // the kernel was leaving (Dekker: it re-reads seq after clearing alive, or this launch serves it)
         const int rc = ll_launch(ll);
@@ -367,16 +417,21 @@ struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll) { return ll->h_d
 uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll) { return ll->h_verd; }
 struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll) { return ll->h_recs; }
 
-int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[12]) {
+// out: [0-3] phase durations, [4-8] wave 0's body stamps, [9] shader MHz, [10-11] host phases (ns);
+// [12-14] poll counts of the running instance -- diagnostics for tools/echo_replay
+int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[15]) {
     xsk_gpu__lowlat* ll = xsk_gpu__ctx_lowlat(ctx);
-    for (int i = 0; i < 12; ++i) out_ns[i] = 0;
+    for (int i = 0; i < 15; ++i) out_ns[i] = 0;
     if (!ll) return -EINVAL;
-    const volatile xsk_gpu__bell* b = ll->h_bell;
-    for (int i = 0; i < 4; ++i) out_ns[i] = b->trace[i] * 10u;
-    for (int i = 0; i < 5; ++i) out_ns[4 + i] = b->body[i] > b->body[5] ? (b->body[i] - b->body[5]) * 10u : 0u;
-    out_ns[9] = b->clk[1] ? b->clk[0] * 100u / b->clk[1] : 0u;  // MHz
+    // a snapshot while the kernel may run on: fields of different batches can mix (diagnostics only)
+    xsk_gpu__lldiag d;
+    if (hipMemcpy(&d, ll->d_diag, sizeof d, hipMemcpyDeviceToHost) != hipSuccess) return -EIO;
+    for (int i = 0; i < 4; ++i) out_ns[i] = d.trace[i] * 10u;
+    for (int i = 0; i < 5; ++i) out_ns[4 + i] = d.body[i] > d.body[5] ? (d.body[i] - d.body[5]) * 10u : 0u;
+    out_ns[9] = d.clk[1] ? d.clk[0] * 100u / d.clk[1] : 0u;  // MHz
     out_ns[10] = ll->host_ns[0];
     out_ns[11] = ll->host_ns[1];
+    for (int i = 0; i < 3; ++i) out_ns[12 + i] = d.polls[i];  // counts, not nanoseconds
     return 0;
 }
 
