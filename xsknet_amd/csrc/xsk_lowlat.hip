@@ -12,12 +12,12 @@
 // Memory ordering (AMDGPU memory model, system scope): the host stores descriptors, then the doorbell
 // sequence number (x86 TSO keeps the order).  Wave 0 of the kernel polls the doorbell with relaxed
 // system-scope loads (two in flight, one per copy of the word); on a new batch it issues ONE system-scope
-// acquire fence, which invalidates the CU's L1 (shared by the workgroup's waves) and the L2 lines of host
-// memory, so recycled UMEM frames are never read stale, then the workgroup meets.  After the body every
-// wave waits for its own stores' acknowledgements, the workgroup meets, and thread 0 issues ONE
-// system-scope release fence (the L2 write-back covers every wave's stores to the UMEM, verdicts and
-// records: one L2 per workgroup) and stores the batch's sequence number to `done`.  (A fence per wave
-// queued sixteen L2 write-backs in front of `done`.)
+// acquire (`buffer_inv sc0 sc1`: the CU's L1, shared by the workgroup's waves, and the L2 lines of host
+// memory, so recycled UMEM frames are never read stale), waits for it, and then the workgroup meets.
+// After the body every wave waits for its own stores' acknowledgements, the workgroup meets, and thread 0
+// issues ONE system-scope release fence (the L2 write-back covers every wave's stores to the UMEM,
+// verdicts and records: one L2 per workgroup), waits for the write-back, and stores the batch's sequence
+// number to `done`.  (A fence per wave queued sixteen L2 write-backs in front of `done`.)
 //
 // Exit conditions every wave reaches: the host's stop word, or no batch for kIdleTicks (50 ms of the
 // 100-MHz wall clock) — so a process that dies without xsk_gpu_fini() never leaves the grid running.
@@ -156,12 +156,12 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                 r = examine(cB, aB, bB);
                 if (r) break;
             }
-            // ONE system-scope acquire for the workgroup (the barrier below orders the other waves after it):
-            // fresh descriptors and frames.  The doorbell read it follows has returned (it was examined);
-            // the other poll may still be in flight and is not waited for (the fence intrinsic would wait
-            // for every outstanding load first: up to half a round trip).  The invalidation travels the
-            // same path as every later load of the workgroup, so none of them can pass it.
-            if (work) asm volatile("buffer_inv sc0 sc1" ::: "memory");
+            // ONE system-scope acquire for the workgroup: fresh descriptors and frames.  The doorbell read it
+            // follows has returned (it was examined).  The invalidation completes asynchronously and only
+            // this wave's own later loads are ordered behind it, so the wave waits for it (and for the other
+            // poll, still in flight: at most half a round trip) before the barrier below releases the
+            // other waves' loads (MI355X_MICROARCH.md, cross-CU hand-off recipe).
+            if (work) asm volatile("buffer_inv sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
             if (n > (uint32_t)XSK_GPU_LOWLAT_MAX) n = XSK_GPU_LOWLAT_MAX;  // the host never posts more
             if (lane == 0) {
                 s_cmd[0] = work;
@@ -212,6 +212,10 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             // system scope, once for the workgroup: write back the L2 lines of host memory the body wrote,
             // wait for it, then publish completion (diagnostics after it: they are not waited for)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            // the write-back must have completed before `done` leaves: ROCm 7.2 drops the fence's own
+            // `s_waitcnt vmcnt(0)` after buffer_wbl2 when this wave's scoreboard is provably empty (it is:
+            // the wait above), and `done` then overtook the verdicts (MI355X_MICROARCH.md, compiler hazard)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint64_t t_end = wall_clock64();
             __hip_atomic_store((uint32_t*)&bell->done, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             // plain stores to device memory: no wait here, acknowledged long before the first poll returns
