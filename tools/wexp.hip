@@ -35,6 +35,11 @@
 //            streams its own 64-frame tile (row q of step s: frame 4s+q), 32 = 31 with each workgroup
 //            starting at a rotated tile of its share, 33 = 30 rotated, 34 = 31 with 512-thread
 //            workgroups (grid 2x), 35 = 31 with 8 loads per lane in flight (two frames per row)
+//   mode 36: 31 with 256-thread workgroups (grid = workgroups); 37: 31 in the wave-front order (pass p: tiles
+//            [p * 16 * grid, ...), wave w of workgroup g tile 16 g + w); 38: 36 in the wave-front order
+//   mode 40-47: the read ladder (wexp_ladder): 40 <4 waves, front, 6 loads>, 41 <16, front, 6>, 42 <16,
+//            contiguous, 6>, 43 <16, contiguous, 4+2>, 44 <16, contiguous, 12 pipelined>, 45 <16, front, 12>,
+//            46 <4, contiguous, 6>, 47 <16, front, 4+2>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(1024) void wexp_rounds(uint8_t* buf, uint32_t n, ui
     }
 }
 
-template <int PAT, bool ROT, int NW>
+template <int PAT, bool ROT, int NW, bool FRONT = false>
 __global__ __launch_bounds__(NW * 64) void wexp_pers(const uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
                                                      unsigned long long* out) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -233,7 +238,8 @@ __global__ __launch_bounds__(NW * 64) void wexp_pers(const uint8_t* buf, uint32_
         }
     } else {  // every wave its own tile
         for (uint32_t c = wave; c < per; c += NW) {
-            const uint32_t t = t0 + (c + rot) % per;
+            // FRONT: the grid's waves sweep the batch in passes of (grid * NW) consecutive tiles
+            const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : t0 + (c + rot) % per;
             if (t >= ntiles) continue;
             for (uint32_t s = 0; s < 16; s += (PAT == 2 ? 2 : 1)) {
                 constexpr int NF = PAT == 2 ? 2 : 1;
@@ -252,6 +258,69 @@ __global__ __launch_bounds__(NW * 64) void wexp_pers(const uint8_t* buf, uint32_
                 for (int h = 0; h < NF; ++h)
 #pragma unroll
                     for (int u = 0; u < 6; ++u) acc += (uint64_t)v[h][u].x + v[h][u].y + v[h][u].z + v[h][u].w;
+            }
+        }
+    }
+    if (acc == 0x123456789ull) out[0] = acc;
+}
+
+// Read ladder (modes 40-46): a clean read-only kernel between wexp_kernel<0> and the round kernel's read
+// pattern.  Frames of a tile are read through a tile-wide raw buffer (out-of-range offsets -> zeros, no
+// branches), 16 lanes per frame (row q of step s: frame 4s+q), 256-B row-loads.  NW waves per workgroup;
+// FRONT: the grid's waves sweep the batch in passes of grid * NW tiles, else contiguous per-workgroup
+// shares; LM 0: a step's 6 row-loads in one batch, 1: batches of 4 + 2 (the shipped U = 4), 2: step
+// s + 1's 6 loads issued before step s is summed (12 in flight).
+template <int NW, bool FRONT, int LM>
+__global__ __launch_bounds__(NW * 64) void wexp_ladder(const uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
+                                                       unsigned long long* out) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    const uint32_t ntiles = (n + 63) / 64;
+    const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+    uint64_t acc = 0;
+    for (uint32_t c = wave; c < per; c += NW) {
+        const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
+        if (t >= ntiles) continue;
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(buf + (uint64_t)t * 64u * stride),
+                                                                           (short)0, (int)(64u * stride), 0x00020000);
+        auto ld = [&](uint32_t s, uint32_t u) -> u32x4 {
+            const uint32_t ro = 256u * u + 16u * k;
+            const uint32_t o = (4u * s + q) * stride + ro;
+            return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(ro < len ? o : 0x80000000u), 0, 2);
+        };
+        if (LM == 2) {
+            u32x4 a[6], b[6];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) a[u] = ld(0, u);
+            for (uint32_t s = 0; s < 16; s += 2) {
+#pragma unroll
+                for (int u = 0; u < 6; ++u) b[u] = ld(s + 1, u);
+#pragma unroll
+                for (int u = 0; u < 6; ++u) acc += (uint64_t)a[u].x + a[u].y + a[u].z + a[u].w;
+                if (s + 2 < 16) {
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) a[u] = ld(s + 2, u);
+                }
+#pragma unroll
+                for (int u = 0; u < 6; ++u) acc += (uint64_t)b[u].x + b[u].y + b[u].z + b[u].w;
+            }
+        } else {
+            for (uint32_t s = 0; s < 16; ++s) {
+                u32x4 v[6];
+                if (LM == 0) {
+#pragma unroll
+                    for (int u = 0; u < 6; ++u) v[u] = ld(s, u);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = ld(s, u);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc += (uint64_t)v[u].x + v[u].y + v[u].z + v[u].w;
+                    v[0] = ld(s, 4);
+                    v[1] = ld(s, 5);
+                    v[2] = v[3] = v[4] = v[5] = u32x4{0, 0, 0, 0};
+                }
+#pragma unroll
+                for (int u = 0; u < 6; ++u) acc += (uint64_t)v[u].x + v[u].y + v[u].z + v[u].w;
             }
         }
     }
@@ -298,6 +367,18 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 33: wexp_pers<0, true, 16><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 34: wexp_pers<1, false, 8><<<2 * grid, 512, 0, s>>>(p, n, stride, len, o); break;
         case 35: wexp_pers<2, false, 16><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        // 36: 31 with 256-thread workgroups (grid = workgroups); 37: 31 in the wave-front order; 38: 36 + front
+        case 36: wexp_pers<1, false, 4><<<g, 256, 0, s>>>(p, n, stride, len, o); break;
+        case 37: wexp_pers<1, false, 16, true><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 38: wexp_pers<1, false, 4, true><<<g, 256, 0, s>>>(p, n, stride, len, o); break;
+        case 40: wexp_ladder<4, true, 0><<<g, 256, 0, s>>>(p, n, stride, len, o); break;
+        case 41: wexp_ladder<16, true, 0><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 42: wexp_ladder<16, false, 0><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 43: wexp_ladder<16, false, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 44: wexp_ladder<16, false, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 45: wexp_ladder<16, true, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 46: wexp_ladder<4, false, 0><<<g, 256, 0, s>>>(p, n, stride, len, o); break;
+        case 47: wexp_ladder<16, true, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 13: wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         case 14: wexp_kernel<14><<<g, b, 0, s>>>(p, n, stride, len, o, side);
                  wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;

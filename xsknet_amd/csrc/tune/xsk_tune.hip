@@ -355,6 +355,12 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             if (!d_workspace) return -EINVAL;
             args.queue = (uint32_t*)((uint8_t*)d_workspace + (768u << 10));
         }
+        if (variant == 103 || variant == 104) {  // 92 in the wave-front tile order (front_mode 1 / 2)
+            const uint32_t ntiles = (n + kTile - 1) / kTile, front = 16u * g6;
+            args.front = front;
+            args.front_mode = variant == 103 ? 1u : 2u;
+            per = 16u * ((ntiles + front - 1) / front);
+        }
         if (variant == 90 || variant == 91) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
             if (!d_workspace) return -EINVAL;
             HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
@@ -405,6 +411,8 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 100: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 16><<<gg, bb, 0, s>>>(args, per); break;
             case 101: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 102: echo_kernel6<4, 2, 2, 2, false, true, false, false, false, true, true, true, false, false, 8><<<gg, bb, 0, s>>>(args, per); break;
+            case 103:
+            case 104: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 82: echo_kernel6<3, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;
             case 83: echo_kernel6<5, 2, 2, 3><<<gg, bb, 0, s>>>(args, per); break;

@@ -46,7 +46,20 @@ struct EchoArgs {
     unsigned long long* trace = nullptr;
     // DLDS kernels only: nonzero = the batch's descriptors (n <= 64) are already in the LDS (Echo6Smem::desc)
     uint32_t desc_in_lds = 0;
+    // round kernel, static shares only: nonzero = the WAVE-FRONT tile order.  The grid's front = 16 * grid
+    // waves sweep the batch in passes of `front` consecutive tiles (pass p: tiles [p * front, p * front +
+    // front)), every wave one tile per pass, so at any moment the whole chip reads one compact region
+    // instead of one separate region per workgroup.  front_mode 1: wave w of workgroup g takes tile
+    // 16 g + w of a pass; 2: tile w * grid + g.  Each workgroup then runs logical tiles [0, 16 * passes).
+    uint32_t front = 0;
+    uint32_t front_mode = 1;
 };
+
+// Physical tile of logical tile lt (lt & 15 = the wave, lt >> 4 = the pass) in the wave-front order.
+__device__ __forceinline__ uint32_t front_tile(const EchoArgs& a, uint32_t lt) {
+    const uint32_t pass = lt >> 4, w = lt & 15u;
+    return pass * a.front + (a.front_mode == 2 ? w * gridDim.x + blockIdx.x : blockIdx.x * 16u + w);
+}
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
 constexpr int kRsrcFlags = 0x00020000;
@@ -1005,13 +1018,17 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         // ================= read phase =================
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const uint32_t t = ub[i] + wave;
+            uint32_t t = ub[i] + wave;
             wbm[i] = 0ull;
             rec[i] = u32x4{0u, 0u, 0u, 0u};
             verd[i] = 0u;
             alo[i] = 0u;
             ahi[i] = 0u;
             if (t >= ue[i]) continue;  // wave-uniform
+            if (!SUBT && !DYN && a.front) {
+                t = front_tile(a, t);
+                if (t >= (a.n + kTile - 1) / kTile) continue;
+            }
             asm volatile("" : "+v"(lane));
             uint8_t* rows = s_hdr[wave][i];
             const uint32_t q = lane >> 4, k = lane & 15u;
@@ -1246,12 +1263,16 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         }
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const uint32_t t = ub[i] + wave;
+            uint32_t t = ub[i] + wave;
             if (NOWR) {  // keep the read phase alive without storing: fold the records into a counter
                 if (t < ue[i]) cnt.rxb += rec[i].x ^ rec[i].w ^ (uint32_t)wbm[i];
                 continue;
             }
             if (t >= ue[i]) continue;
+            if (!SUBT && !DYN && a.front) {
+                t = front_tile(a, t);
+                if (t >= (a.n + kTile - 1) / kTile) continue;
+            }
             const uint8_t* rows = s_hdr[wave][i];
             if (wbm[i]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
 #pragma unroll
@@ -1318,8 +1339,9 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     if (TAIL == 0) {
-        const uint32_t t_begin = blockIdx.x * tiles_per_wg;
-        const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+        // wave-front order (a.front): every workgroup runs logical tiles [0, tiles_per_wg = 16 * passes)
+        const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
+        const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN>(a, t_begin, t_end,
                                                                                             tiles_per_wg, sm);
         return;
