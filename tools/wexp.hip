@@ -40,6 +40,9 @@
 //   mode 40-47: the read ladder (wexp_ladder): 40 <4 waves, front, 6 loads>, 41 <16, front, 6>, 42 <16,
 //            contiguous, 6>, 43 <16, contiguous, 4+2>, 44 <16, contiguous, 12 pipelined>, 45 <16, front, 12>,
 //            46 <4, contiguous, 6>, 47 <16, front, 4+2>
+//   mode 50-53: two-phase (12) with Infinity-Cache policies for the window line in the first pass: 50 the
+//            first 128-B line default-policy, the rest nt; 51 everything default; 52 = 50 via raw buffer
+//            loads; 53 = 50's first pass alone
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -79,7 +82,11 @@ __global__ __launch_bounds__(256) void wexp_kernel(uint8_t* buf, uint32_t n, uin
                     const uint32_t ro = 256u * u + 16u * k;
                     v[u] = u32x4{0, 0, 0, 0};
                     if (ro < len) {
-                        if (MODE == 6 || (MODE == 14 && u == 0 && k < 4)) v[u] = *(const u32x4*)(fr + ro);
+                        if (MODE == 6 || MODE == 51 || (MODE == 14 && u == 0 && k < 4) || (MODE == 50 && u == 0 && k < 8))
+                            v[u] = *(const u32x4*)(fr + ro);
+                        else if (MODE == 52 && u == 0 && k < 8)
+                            v[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                                __builtin_amdgcn_make_buffer_rsrc((void*)fr, (short)0, 256, 0x00020000), (int)ro, 0, 0);
                         else v[u] = __builtin_nontemporal_load((const u32x4*)(fr + ro));
                     }
                 }
@@ -382,6 +389,16 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 13: wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         case 14: wexp_kernel<14><<<g, b, 0, s>>>(p, n, stride, len, o, side);
                  wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
+        // 50-52: two-phase (12) with the first pass loading each frame's first 128-B line with the default
+        // policy (50; 52: a raw buffer load, aux 0) and the rest nontemporal, or everything default (51):
+        // can the windows stay in the Infinity Cache for the second pass?
+        case 50: wexp_kernel<50><<<g, b, 0, s>>>(p, n, stride, len, o, side);
+                 wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
+        case 51: wexp_kernel<51><<<g, b, 0, s>>>(p, n, stride, len, o, side);
+                 wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
+        case 52: wexp_kernel<52><<<g, b, 0, s>>>(p, n, stride, len, o, side);
+                 wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
+        case 53: wexp_kernel<50><<<g, b, 0, s>>>(p, n, stride, len, o, side); break;  // 50's first pass alone
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -411,6 +411,11 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 100: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 16><<<gg, bb, 0, s>>>(args, per); break;
             case 101: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 4><<<gg, bb, 0, s>>>(args, per); break;
             case 102: echo_kernel6<4, 2, 2, 2, false, true, false, false, false, true, true, true, false, false, 8><<<gg, bb, 0, s>>>(args, per); break;
+            // 105: 92 without the write phase (read phase alone, wrong results); 106: 105 with no round
+            // waits (SYNC 0); 107: 92 with SYNC 0 (every wave writes as soon as it has read)
+            case 105: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 106: echo_kernel6<4, 2, 0, 2, false, false, false, false, true, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 107: echo_kernel6<4, 2, 0, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 103:
             case 104: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;

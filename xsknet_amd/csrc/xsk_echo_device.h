@@ -847,7 +847,7 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
 }
 
 // SYNC: how a wave enters its write phase.  0: at once; 1: workgroup barrier (all waves read, then
-// all write); 2: a wave whose tiles averaged >= kHeavyLen bytes per frame waits until every wave of
+// all write); 2: a wave at least half of whose frames this round had >= kHeavyLen bytes waits until every wave of
 // the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
 // phase separation pays where reads dominate, and costs latency hiding where frames are short.
 // 3 / 4 (tuning only): a chip-wide barrier before (3) or around (4) every write phase, on a counter the
@@ -1014,7 +1014,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         u32x4 rec[TPW];
         uint32_t verd[TPW], alo[TPW], ahi[TPW];
         uint64_t wbm[TPW];
-        uint32_t round_bytes = 0;  // SYNC 2: frame bytes this wave read this round (wave-uniform)
+        uint32_t round_long = 0;  // SYNC 2: frames of >= kHeavyLen bytes this wave read this round (uniform)
         // ================= read phase =================
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
@@ -1085,7 +1085,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             }
             alo[i] = dsc.x;
             ahi[i] = dsc.y;
-            if (SYNC == 2) round_bytes += wave_sum_u32(in_n ? min(len, 65536u) : 0u);
+            if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= kHeavyLen));
 
             if (TRACE && threadIdx.x == 0 && i == 0) a.trace[0] = wall_clock64();  // descriptors parsed
             // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
@@ -1255,7 +1255,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         if (SYNC == 2) {
             ++rounds_done;
             if (lane == 0) atomicAdd(&s_arrive, 1u);
-            if (uniform(round_bytes) >= kHeavyLen * kTile * TPW) {
+            if (uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
                 while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
                        rounds_done * (uint32_t)kWaves6)
                     __builtin_amdgcn_s_sleep(2);
