@@ -267,6 +267,9 @@ def main():
     ap.add_argument("--pool-cap", type=int, default=0, help="cap the batch pool (rehearsals on a shared GPU)")
     ap.add_argument("--alloc", default="slab", choices=("slab", "separate"),
                     help="batch pool as one device allocation (slab, like one UMEM region) or one per batch")
+    ap.add_argument("--variant", type=int, default=-1,
+                    help="A/B only: time tuning-library kernel variant N (tools/kbench.py numbering) instead of the "
+                         "shipped entry point; the line is marked and is never the bench value")
     ap.add_argument("--opts", type=int, default=0,
                     help="wire-format options (XSK_GPU_OPT_*, xsk_gpu_echo_dev_opts); 0 = the reference's gates")
     args = ap.parse_args()
@@ -331,12 +334,21 @@ def main():
     ws = torch.zeros(max(16, X.workspace_size(local, n)), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    tune = X.tune_lib() if args.variant >= 0 else None
+    wsv = torch.zeros(1 << 20, dtype=torch.uint8, device=dev) if args.variant >= 0 else None
+
     def step(s):
         b = s % pool
         verd = verds[b % len(verds)]
         if rearm_in_loop and s >= pool:
             X.rearm_dev(umems[b], descss[b], verd, n, stream)  # conservative: counted inside the timing
-        X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream, opts=args.opts)
+        if args.variant >= 0:  # A/B timing of a tuning variant (counters as per-workgroup partials in ws)
+            rc = tune.xsk_gpu__echo_variant(args.variant, 0, umems[b].data_ptr(), umems[b].numel(),
+                                            descss[b].data_ptr(), n, verd.data_ptr(), recs.data_ptr(), wsv.data_ptr(),
+                                            stream.cuda_stream)
+            assert rc == 0, rc
+        else:
+            X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream, opts=args.opts)
 
     for s in range(W):
         step(s)
@@ -372,7 +384,7 @@ def main():
 
     # ---- correctness of what was timed: every frame of every step accepted and counted ----
     st = stats.cpu().numpy().view(X.STATS_DTYPE)[0]
-    ok = int(st["rx_packets"]) == (W + K) * n and int(st["tx_packets"]) == (W + K) * n
+    ok = args.variant >= 0 or (int(st["rx_packets"]) == (W + K) * n and int(st["tx_packets"]) == (W + K) * n)
     ok = ok and all(bool((v == 0).all().item()) for v in verds)
     recs_np = recs.cpu().numpy().view(X.REC_DTYPE)
     ok = ok and bool((recs_np["flags"] == 3).all())
@@ -420,6 +432,8 @@ def main():
                        "layout": "device-resident UMEM slab + xdp_desc array", "pool_alloc": args.alloc,
                        "rearm_in_timed_region": rearm_in_loop},
             "verified": bool(ok_all == world),
+            **({"ab_variant": args.variant, "note": "A/B timing of a tuning variant, not the shipped kernel"}
+               if args.variant >= 0 else {}),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config, kernel) if args.opts == 0 else None,
                          "kernel": kernel, "kernel_avg_us": round(kern_avg_ms * 1e3, 2), "kernel_timer": timer_src,

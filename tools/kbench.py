@@ -90,7 +90,7 @@ def main():
                             assert rc == 0, rc
                         ev1.record()
                         evs.append((ev0, ev1))
-                    if (0 <= v < 10 or v >= 20) and v not in (85, 105, 106):  # NOWR variants write nothing: nothing to re-arm
+                    if (0 <= v < 10 or v >= 20) and v not in (85, 105, 106, 109, 114, 115):  # NOWR variants write nothing: nothing to re-arm
                         for b in range(pool):
                             X.rearm_dev(umems[b], descss[b], verds[b], n)
                     if rep > 0:

@@ -43,6 +43,11 @@
 //   mode 50-53: two-phase (12) with Infinity-Cache policies for the window line in the first pass: 50 the
 //            first 128-B line default-policy, the rest nt; 51 everything default; 52 = 50 via raw buffer
 //            loads; 53 = 50's first pass alone
+//   mode 60-64: ladder with 8 waves (512-thread workgroups): 60 <8, contiguous, 12 pipelined>, 61 <8, contiguous,
+//            6>; and with every window written once at the END of the workgroup's share (ENDW): 62 <16,
+//            contiguous, 4+2>, 63 <8, contiguous, 12>, 64 <16, contiguous, 12>; 65: 62 with the windows of
+//            every 2 tiles of a wave written after them (2 write phases per share, no sync); 66: 65 with a
+//            workgroup barrier before each write phase
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -277,8 +282,8 @@ __global__ __launch_bounds__(NW * 64) void wexp_pers(const uint8_t* buf, uint32_
 // FRONT: the grid's waves sweep the batch in passes of grid * NW tiles, else contiguous per-workgroup
 // shares; LM 0: a step's 6 row-loads in one batch, 1: batches of 4 + 2 (the shipped U = 4), 2: step
 // s + 1's 6 loads issued before step s is summed (12 in flight).
-template <int NW, bool FRONT, int LM>
-__global__ __launch_bounds__(NW * 64) void wexp_ladder(const uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
+template <int NW, bool FRONT, int LM, int ENDW = 0>
+__global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
                                                        unsigned long long* out) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 4, k = lane & 15u;
@@ -287,6 +292,18 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(const uint8_t* buf, uint3
     uint64_t acc = 0;
     for (uint32_t c = wave; c < per; c += NW) {
         const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
+        if (ENDW >= 2 && c >= 2u * NW && ((c / NW) & 1u) == 0u) {  // a write phase after every 2 tiles
+            if (ENDW == 3) __syncthreads();
+            const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
+            for (uint32_t cc = c - 2u * NW; cc < c; cc += NW) {
+                const uint32_t tt = blockIdx.x * per + cc;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const uint32_t f = tt * 64u + (uint32_t)rr * 16u + (lane >> 2);
+                    if (tt < ntiles && f < n) *(u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u)) = w;
+                }
+            }
+        }
         if (t >= ntiles) continue;
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(buf + (uint64_t)t * 64u * stride),
                                                                            (short)0, (int)(64u * stride), 0x00020000);
@@ -328,6 +345,19 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(const uint8_t* buf, uint3
                 }
 #pragma unroll
                 for (int u = 0; u < 6; ++u) acc += (uint64_t)v[u].x + v[u].y + v[u].z + v[u].w;
+            }
+        }
+    }
+    if (ENDW) {  // every frame's 64-B window written once, after the workgroup has read its whole share
+        if (ENDW != 2) __syncthreads();
+        const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
+        for (uint32_t c = ENDW >= 2 ? wave + ((per - wave + NW - 1) / NW - 1) / 2 * 2 * NW : wave; c < per; c += NW) {
+            const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
+            if (t >= ntiles) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t f = t * 64u + (uint32_t)r * 16u + (lane >> 2);
+                if (f < n) *(u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u)) = w;
             }
         }
     }
@@ -386,6 +416,13 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 45: wexp_ladder<16, true, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 46: wexp_ladder<4, false, 0><<<g, 256, 0, s>>>(p, n, stride, len, o); break;
         case 47: wexp_ladder<16, true, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 60: wexp_ladder<8, false, 2><<<g, 512, 0, s>>>(p, n, stride, len, o); break;
+        case 61: wexp_ladder<8, false, 0><<<g, 512, 0, s>>>(p, n, stride, len, o); break;
+        case 62: wexp_ladder<16, false, 1, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 63: wexp_ladder<8, false, 2, 1><<<g, 512, 0, s>>>(p, n, stride, len, o); break;
+        case 64: wexp_ladder<16, false, 2, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 65: wexp_ladder<16, false, 1, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 66: wexp_ladder<16, false, 1, 3><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 13: wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         case 14: wexp_kernel<14><<<g, b, 0, s>>>(p, n, stride, len, o, side);
                  wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;

@@ -416,6 +416,22 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 105: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 106: echo_kernel6<4, 2, 0, 2, false, false, false, false, true, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 107: echo_kernel6<4, 2, 0, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 108-111: the one-round kernel echo_kernel8 (8 waves, TPW tiles per wave, VT of them in VGPRs):
+            // 108 <4, 8, 4> SYNC 0; 109 = 108 NOWR; 110 <4, 8, 4> SYNC 2; 111 <4, 4, 0> (LDS only, 2 rounds at c3)
+            case 108: echo_kernel8<4, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 109: echo_kernel8<4, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 110: echo_kernel8<4, 8, 4, 2><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 111: echo_kernel8<4, 4, 0><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            // 112 / 113: 108 with 6 / 8 row-loads in flight per lane; 114 / 115 their read phases alone
+            // 116: 92 with the next tile's descriptors prefetched while the current one streams (PF)
+            case 116: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 117 / 118: 92 with software-pipelined ranked streams for every tile (STREAM 3) / ragged tiles (4)
+            case 117: echo_kernel6<4, 2, 2, 3, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 118: echo_kernel6<4, 2, 2, 4, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 115: echo_kernel8<8, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 103:
             case 104: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 81: echo_kernel6<4, 2, 2, 4><<<gg, bb, 0, s>>>(args, per); break;

@@ -931,15 +931,16 @@ struct DynQueue {
     }
 };
 
-// LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB in reference mode).
-template <int TPW, bool WIRE, int STREAM>
+// LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB in reference mode).  NW waves, SLOTS
+// LDS header-window tiles per wave (= TPW unless some tiles of a round are held in VGPRs, echo6_body VT).
+template <int TPW, bool WIRE, int STREAM, int NW = kWaves6, int SLOTS = TPW>
 struct Echo6Smem {
     static constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;
-    __attribute__((aligned(16))) uint8_t hdr[kWaves6][TPW][kTile * kRowW];  // 128 KiB: header windows
-    __attribute__((aligned(16))) FrameMeta6 meta[kWaves6][kTile];          // 16 KiB
-    uint32_t sum[kWaves6][2][kTile];                                        // 8 KiB
-    uint32_t sort[STREAM >= 1 ? kWaves6 : 1][80];                          // 5 KiB (STREAM 1, 2)
-    unsigned long long cnt[kWaves6][4];
+    __attribute__((aligned(16))) uint8_t hdr[NW][SLOTS][kTile * kRowW];  // 128 KiB: header windows
+    __attribute__((aligned(16))) FrameMeta6 meta[NW][kTile];            // 16 KiB (NW 16)
+    uint32_t sum[NW][2][kTile];                                          // 8 KiB
+    uint32_t sort[STREAM >= 1 ? NW : 1][80];                            // 5 KiB (STREAM 1, 2)
+    unsigned long long cnt[NW][4];
     uint32_t arrive;
     uint32_t claim[TPW][2];  // DYN: this round's units [begin, end) in tiles
     u32x4 desc[kTile];       // DLDS: the descriptors of a batch of <= 64 frames, delivered with its doorbell
@@ -949,13 +950,18 @@ struct Echo6Smem {
 // workgroup calls it with the same range): rounds of kWaves6 * TPW tiles, read phase, write phase, and
 // the counters (store_partials).  echo_kernel6 runs it once per workgroup on its static share; the
 // low-latency persistent kernel (xsk_lowlat.hip) once per doorbell.
+// NW: waves per workgroup.  VT: the first VT tiles of a wave's round keep their patched header windows in
+// VGPRs (lane = frame, 64 B) instead of an LDS slot -- they stream through slot 0 and are copied out after
+// their header phase -- so a round holds TPW tiles per wave in TPW - VT LDS slots (the one-round kernel,
+// echo_kernel8: 8 waves x 8 tiles = a whole 4096-frame CU share, written in ONE write phase at its end).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, bool TRACE = false, bool DLDS = false>
+          bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
-                                           Echo6Smem<TPW, WIRE, STREAM>& sm) {
-    static_assert(!DYN || (!PF && SYNC < 3 && !SUBT), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
+                                           Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
+    static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
+    static_assert(VT == 0 || (!WIRE && !PF && TPW - VT >= 1 && VT <= TPW - VT), "VGPR tiles: reference mode, LDS slots for them to pass through");
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;  // LDS row (header window) bytes
     const uint64_t wgt_start = WGT ? wall_clock64() : 0ull;
     auto& s_hdr = sm.hdr;
@@ -972,7 +978,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     FrameMeta6* meta = sm.meta[wave];
     uint32_t* sums_ic = sm.sum[wave][0];
     uint32_t* sums_ip = sm.sum[wave][1];
-    constexpr uint32_t kRound = (uint32_t)kWaves6 * TPW;
+    constexpr uint32_t kRound = (uint32_t)NW * TPW;
     Counters cnt;
     uint32_t lane = threadIdx.x & 63u;
     u32x4 dnext = u32x4{0u, 0u, 0u, 0u};  // PF: descriptor of this lane's frame in the wave's next tile
@@ -1006,235 +1012,283 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             if (r0 >= r_end) break;
 #pragma unroll
             for (int i = 0; i < TPW; ++i) {
-                ub[i] = r0 + (uint32_t)i * kWaves6;
+                ub[i] = r0 + (uint32_t)i * NW;
                 ue[i] = t_end;
             }
             r0 += kRound;
         }
         u32x4 rec[TPW];
+        u32x4 vwin[VT > 0 ? VT : 1][4];  // VT: patched windows of the VGPR tiles (lane = frame, 64 B)
         uint32_t verd[TPW], alo[TPW], ahi[TPW];
         uint64_t wbm[TPW];
         uint32_t round_long = 0;  // SYNC 2: frames of >= kHeavyLen bytes this wave read this round (uniform)
         // ================= read phase =================
-#pragma unroll
+        // VT == 0: the TPW slots unrolled, every tile's outputs straight into the per-slot arrays; VT > 0 (8
+        // tiles per wave): a rolled loop whose outputs are pushed onto register queues with constant indices
+        // (dynamically indexed VGPR arrays would live in scratch memory)
+        constexpr int kReadUnroll = VT > 0 ? 1 : TPW;
+#pragma unroll kReadUnroll
         for (int i = 0; i < TPW; ++i) {
-            uint32_t t = ub[i] + wave;
-            wbm[i] = 0ull;
-            rec[i] = u32x4{0u, 0u, 0u, 0u};
-            verd[i] = 0u;
-            alo[i] = 0u;
-            ahi[i] = 0u;
-            if (t >= ue[i]) continue;  // wave-uniform
-            if (!SUBT && !DYN && a.front) {
-                t = front_tile(a, t);
-                if (t >= (a.n + kTile - 1) / kTile) continue;
-            }
-            asm volatile("" : "+v"(lane));
-            uint8_t* rows = s_hdr[wave][i];
-            const uint32_t q = lane >> 4, k = lane & 15u;
-            static_assert(!(SUBT && PF), "sub-tiles take no descriptor prefetch");
-            const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
-            const bool in_n = (!SUBT || lane < a.tile_live) && fi < a.n;  // a live frame of the batch
-            // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
-            u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
-            if (PF) {
-                dsc = dnext;
-                const uint32_t tn = i + 1 < TPW ? t + (uint32_t)kWaves6 : r0 + wave;  // next tile (r0: next round)
-                const uint32_t fn = tn * kTile + lane;
-                dnext = u32x4{0u, 0u, 0u, 0u};
-                if (tn < t_end && fn < a.n) dnext = *(const u32x4*)(a.descs + fn);
-            } else if (DLDS && a.desc_in_lds) {
-                if (in_n) dsc = sm.desc[fi];  // n <= 64: fi < 64
-            } else if (in_n) {
-                dsc = *(const u32x4*)(a.descs + fi);
-            }
-            const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
-            const uint32_t len = dsc.z;
-            // reference mode reads bytes [0, 38) whenever len >= 20 (xsk_receive.c:120-157); wire mode
-            // reads only [addr, addr + len) plus the window
-            const uint64_t need = WIRE ? len : (len >= 20 ? (len > 38 ? len : 38) : len);
-            const bool ok = in_n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
-            const bool parse = ok && len >= (WIRE ? 14u : 20u);
-            const uint64_t a16 = addr & ~15ull;
-            const uint32_t off = (uint32_t)addr & 15u;
-            const uint32_t rowhi = parse ? off + len : 0u;
-            const uint32_t wend = ok ? (uint32_t)min(a.umem_size - a16, (uint64_t)kRowW) : 0u;
-            const uint32_t win = parse ? wend : 0u;
-            const uint32_t lim = max(rowhi, win);
-            const uint32_t nit = (lim + 255u) >> 8;
-            const bool short_tile = __ballot(lim > kRowW) == 0ull;
-            const bool mid_tile = MID && !WIRE && !short_tile && __ballot(lim > 128u) == 0ull;
-            // SKM: every frame of the tile at the same 16-B offset with the same end (c2, pings): the ICMP
-            // byte masks of a lane's block are the same for all its frames -> computed once per tile
-            const uint32_t ukey = (off << 24) ^ rowhi;
-            const bool uni_tile = SKM && !WIRE && (short_tile || mid_tile) && __ballot(ukey != uniform(ukey)) == 0ull;
-            uint64_t wlo = 0, span = ~0ull;
-            if (!short_tile) {
-                wlo = wave_min_u64(nit ? a16 : ~0ull);
-                span = wave_max_u64(nit ? a16 + lim : 0ull) - wlo;
-            }
-            const bool fast = !short_tile && !mid_tile && span < 0x80000000ull;  // wave-uniform
-            {
-                FrameMeta6 m;
-                m.rel = fast ? (nit ? (uint32_t)(a16 - wlo) : 0u) : (uint32_t)(a16 >> 4);
-                m.rowhi = rowhi;
-                m.lim = lim;
-                m.packed = off | ((parse ? off + min(len, 34u) : 0u) << 8) | ((ok ? 1u : 0u) << 16) |
-                           ((parse ? 2u : 0u) << 16) | ((uint32_t)(a16 >> 36) << 20);
-                meta[lane] = m;
-            }
-            alo[i] = dsc.x;
-            ahi[i] = dsc.y;
-            if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= kHeavyLen));
+            const uint32_t ub_i = VT > 0 ? ub[0] + (uint32_t)i * NW : ub[i], ue_i = VT > 0 ? ue[0] : ue[i];
+            u32x4 rec_o;
+            uint32_t verd_o, alo_o, ahi_o;
+            uint64_t wbm_o;
+            u32x4 vcur[4];
+            do {  // one tile; `break` = the slot has no tile for this wave
+                uint32_t t = ub_i + wave;
+                wbm_o = 0ull;
+                rec_o = u32x4{0u, 0u, 0u, 0u};
+                verd_o = 0u;
+                alo_o = 0u;
+                ahi_o = 0u;
+                if (t >= ue_i) break;  // wave-uniform
+                if (!SUBT && !DYN && a.front) {
+                    t = front_tile(a, t);
+                    if (t >= (a.n + kTile - 1) / kTile) break;
+                }
+                asm volatile("" : "+v"(lane));
+                uint8_t* rows = s_hdr[wave][i < VT ? 0 : i - VT];  // VGPR tiles pass through slot 0
+                const uint32_t q = lane >> 4, k = lane & 15u;
+                static_assert(!(SUBT && PF), "sub-tiles take no descriptor prefetch");
+                const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
+                const bool in_n = (!SUBT || lane < a.tile_live) && fi < a.n;  // a live frame of the batch
+                // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
+                u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
+                if (PF) {
+                    dsc = dnext;
+                    const uint32_t tn = i + 1 < TPW ? t + (uint32_t)NW : r0 + wave;  // next tile (r0: next round)
+                    const uint32_t fn = tn * kTile + lane;
+                    dnext = u32x4{0u, 0u, 0u, 0u};
+                    if (tn < t_end && fn < a.n) dnext = *(const u32x4*)(a.descs + fn);
+                } else if (DLDS && a.desc_in_lds) {
+                    if (in_n) dsc = sm.desc[fi];  // n <= 64: fi < 64
+                } else if (in_n) {
+                    dsc = *(const u32x4*)(a.descs + fi);
+                }
+                const uint64_t addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
+                const uint32_t len = dsc.z;
+                // reference mode reads bytes [0, 38) whenever len >= 20 (xsk_receive.c:120-157); wire mode
+                // reads only [addr, addr + len) plus the window
+                const uint64_t need = WIRE ? len : (len >= 20 ? (len > 38 ? len : 38) : len);
+                const bool ok = in_n && len <= kMaxLen && addr <= a.umem_size && need <= a.umem_size - addr;
+                const bool parse = ok && len >= (WIRE ? 14u : 20u);
+                const uint64_t a16 = addr & ~15ull;
+                const uint32_t off = (uint32_t)addr & 15u;
+                const uint32_t rowhi = parse ? off + len : 0u;
+                const uint32_t wend = ok ? (uint32_t)min(a.umem_size - a16, (uint64_t)kRowW) : 0u;
+                const uint32_t win = parse ? wend : 0u;
+                const uint32_t lim = max(rowhi, win);
+                const uint32_t nit = (lim + 255u) >> 8;
+                const bool short_tile = __ballot(lim > kRowW) == 0ull;
+                const bool mid_tile = MID && !WIRE && !short_tile && __ballot(lim > 128u) == 0ull;
+                // SKM: every frame of the tile at the same 16-B offset with the same end (c2, pings): the ICMP
+                // byte masks of a lane's block are the same for all its frames -> computed once per tile
+                const uint32_t ukey = (off << 24) ^ rowhi;
+                const bool uni_tile = SKM && !WIRE && (short_tile || mid_tile) && __ballot(ukey != uniform(ukey)) == 0ull;
+                uint64_t wlo = 0, span = ~0ull;
+                if (!short_tile) {
+                    wlo = wave_min_u64(nit ? a16 : ~0ull);
+                    span = wave_max_u64(nit ? a16 + lim : 0ull) - wlo;
+                }
+                const bool fast = !short_tile && !mid_tile && span < 0x80000000ull;  // wave-uniform
+                {
+                    FrameMeta6 m;
+                    m.rel = fast ? (nit ? (uint32_t)(a16 - wlo) : 0u) : (uint32_t)(a16 >> 4);
+                    m.rowhi = rowhi;
+                    m.lim = lim;
+                    m.packed = off | ((parse ? off + min(len, 34u) : 0u) << 8) | ((ok ? 1u : 0u) << 16) |
+                               ((parse ? 2u : 0u) << 16) | ((uint32_t)(a16 >> 36) << 20);
+                    meta[lane] = m;
+                }
+                alo_o = dsc.x;
+                ahi_o = dsc.y;
+                if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= kHeavyLen));
 
-            if (TRACE && threadIdx.x == 0 && i == 0) a.trace[0] = wall_clock64();  // descriptors parsed
-            // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
-            if (__ballot(nit != 0u) != 0ull) {
-                __builtin_amdgcn_wave_barrier();
-                WinLoader ld;
-                ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
-                                                         fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
-                if (WIRE && short_tile) {
-                    // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
-                    // nothing lies past byte 128, so the streamed part of every sum is zero
-                    const uint32_t kk = lane & 7u, ro = 16u * kk;
-                    u32x4 x[8];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
-                        const bool in = ro < fm.lim;
-                        x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
-                        if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
-                    }
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
-                        const u32x4 v = ro < meta[f].lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
-                        *(u32x4*)(rows + f * kRowW + ro) = v;
-                    }
-                    sums_ic[lane] = 0u;
-                } else if (short_tile) {
-                    // every frame within its 64-B window: 4 lanes per frame, 16 frames per wave-load
-                    const uint32_t kk = lane & 3u, ro = 16u * kk;
-                    const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
-                    u32x4 x[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const FrameMeta6& fm = meta[(uint32_t)r * 16u + (lane >> 2)];
-                        const bool in = ro < fm.lim;
-                        x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
-                        if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
-                    }
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
-                        const FrameMeta6& fm = meta[f];
-                        const uint32_t f_packed = fm.packed;
-                        const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
-                        *(u32x4*)(rows + f * kRowW + ro) = v;
-                        const int f_off = (int)(f_packed & 0xFFu), f_iphi = (int)((f_packed >> 8) & 0xFFu);
-                        // D2: the IPv4 header sum comes from the window in the header phase (STREAM >= 1)
-                        constexpr bool kRip = !(D2 && STREAM >= 1);
-                        uint32_t rip = 0u;
-                        if (kRip) rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
-                        uint32_t ric = (SKM && uni_tile) ? sum_halves(v & umk, 0u)
-                                     : D2 ? sum_range_h(v, (int)ro, f_off + 34, (int)fm.rowhi)
-                                          : fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
-                        if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);
-                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);
-                        if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0x4E, 0xF, 0xF, false);
-                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);
-                        if (kk == 0u) {
-                            sums_ic[f] = ric;
-                            if (kRip) sums_ip[f] = rip;
+                if (TRACE && threadIdx.x == 0 && i == 0) a.trace[0] = wall_clock64();  // descriptors parsed
+                // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
+                if (__ballot(nit != 0u) != 0ull) {
+                    __builtin_amdgcn_wave_barrier();
+                    WinLoader ld;
+                    ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
+                                                             fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
+                    if (WIRE && short_tile) {
+                        // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
+                        // nothing lies past byte 128, so the streamed part of every sum is zero
+                        const uint32_t kk = lane & 7u, ro = 16u * kk;
+                        u32x4 x[8];
+    #pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
+                            const bool in = ro < fm.lim;
+                            x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
+                            if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
                         }
-                    }
-                } else if (MID && !WIRE && mid_tile) {
-                    // every frame within 128 B of its 16-B aligned start (pings): 8 lanes per frame, 8 frames
-                    // per wave-load, all 8 loads in flight at once; the ICMP sum by exact byte range, reduced
-                    // over the 8 lanes (the IPv4 header sum comes from the window in the header phase)
-                    const uint32_t kk = lane & 7u, ro = 16u * kk;
-                    const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
-                    u32x4 x[8];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
-                        const bool in = ro < fm.lim;
-                        x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
-                        if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
-                    }
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) {
-                        const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
-                        const FrameMeta6& fm = meta[f];
-                        const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
-                        if (kk < 4u) *(u32x4*)(rows + f * kRowW + ro) = v;
-                        uint32_t ric = (SKM && uni_tile) ? sum_halves(v & umk, 0u)
-                                     : D2 ? sum_range_h(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi)
-                                          : fold64(sum_range(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi));
-                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);   // xor 1
-                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);   // xor 2
-                        ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x141, 0xF, 0xF, false);  // half-row mirror
-                        if (kk == 0u) sums_ic[f] = ric;
-                    }
-                } else if (STREAM == 3 ||
-                           (STREAM == 4 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
-                                            uniform(max_nit_lane(nit)) < (uint32_t)U))) {
-                    static_assert(!WIRE || STREAM < 3, "wire mode uses the non-pipelined streams");
-                    if (fast) stream_tile_sorted_pl<U, true>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted_pl<U, false>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                } else if (STREAM == 1 ||
-                           (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
-                                            uniform(max_nit_lane(nit)) < (uint32_t)U))) {
-                    // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
-                    if (fast) stream_tile_sorted<U, true, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    else stream_tile_sorted<U, false, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                } else {
-                    for (uint32_t s = 0; s < 16; ++s) {
-                        const uint32_t f = 4u * s + q;
-                        const FrameMeta6& fm = meta[f];  // broadcast read: one entry per 16-lane row
-                        const uint32_t f_lim = fm.lim;
-                        const uint32_t f_nit = (f_lim + 255u) >> 8;
-                        const uint32_t ns = max(max(rdlane(f_nit, 0), rdlane(f_nit, 16)),
-                                                max(rdlane(f_nit, 32), rdlane(f_nit, 48)));
-                        if (ns == 0) continue;
-                        const uint32_t f_rowhi = fm.rowhi, f_packed = fm.packed;
-                        const uint32_t f_off = f_packed & 0xFFu, f_iphi = (f_packed >> 8) & 0xFFu;
-                        RowSums rs;
-                        if (fast) {
-                            ld.rel = fm.rel;
-                            stream_frame<U, WinLoader, WIRE, D2>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
-                        } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
-                            FarLoader fl;
-                            fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
-                            stream_frame<U, FarLoader, WIRE, D2>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+    #pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
+                            const u32x4 v = ro < meta[f].lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                            *(u32x4*)(rows + f * kRowW + ro) = v;
                         }
-                        const uint32_t ric = row_sum_dpp(fold64(rs.ic));
-                        const uint32_t rip = row_sum_dpp(fold64(rs.ip));
-                        if (k == 15u) {
-                            sums_ic[f] = ric;
-                            sums_ip[f] = rip;
+                        sums_ic[lane] = 0u;
+                    } else if (short_tile) {
+                        // every frame within its 64-B window: 4 lanes per frame, 16 frames per wave-load
+                        const uint32_t kk = lane & 3u, ro = 16u * kk;
+                        const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
+                        u32x4 x[4];
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const FrameMeta6& fm = meta[(uint32_t)r * 16u + (lane >> 2)];
+                            const bool in = ro < fm.lim;
+                            x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
+                            if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
+                        }
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                            const FrameMeta6& fm = meta[f];
+                            const uint32_t f_packed = fm.packed;
+                            const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                            *(u32x4*)(rows + f * kRowW + ro) = v;
+                            const int f_off = (int)(f_packed & 0xFFu), f_iphi = (int)((f_packed >> 8) & 0xFFu);
+                            // D2: the IPv4 header sum comes from the window in the header phase (STREAM >= 1)
+                            constexpr bool kRip = !(D2 && STREAM >= 1);
+                            uint32_t rip = 0u;
+                            if (kRip) rip = fold64(sum_range(v, (int)ro, f_off + 14, f_iphi));
+                            uint32_t ric = (SKM && uni_tile) ? sum_halves(v & umk, 0u)
+                                         : D2 ? sum_range_h(v, (int)ro, f_off + 34, (int)fm.rowhi)
+                                              : fold64(sum_range(v, (int)ro, f_off + 34, (int)fm.rowhi));
+                            if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0xB1, 0xF, 0xF, false);
+                            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);
+                            if (kRip) rip += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rip, 0x4E, 0xF, 0xF, false);
+                            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);
+                            if (kk == 0u) {
+                                sums_ic[f] = ric;
+                                if (kRip) sums_ip[f] = rip;
+                            }
+                        }
+                    } else if (MID && !WIRE && mid_tile) {
+                        // every frame within 128 B of its 16-B aligned start (pings): 8 lanes per frame, 8 frames
+                        // per wave-load, all 8 loads in flight at once; the ICMP sum by exact byte range, reduced
+                        // over the 8 lanes (the IPv4 header sum comes from the window in the header phase)
+                        const uint32_t kk = lane & 7u, ro = 16u * kk;
+                        const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
+                        u32x4 x[8];
+    #pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
+                            const bool in = ro < fm.lim;
+                            x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
+                            if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
+                        }
+    #pragma unroll
+                        for (int r = 0; r < 8; ++r) {
+                            const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
+                            const FrameMeta6& fm = meta[f];
+                            const u32x4 v = ro < fm.lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
+                            if (kk < 4u) *(u32x4*)(rows + f * kRowW + ro) = v;
+                            uint32_t ric = (SKM && uni_tile) ? sum_halves(v & umk, 0u)
+                                         : D2 ? sum_range_h(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi)
+                                              : fold64(sum_range(v, (int)ro, (int)(fm.packed & 0xFFu) + 34, (int)fm.rowhi));
+                            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);   // xor 1
+                            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);   // xor 2
+                            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x141, 0xF, 0xF, false);  // half-row mirror
+                            if (kk == 0u) sums_ic[f] = ric;
+                        }
+                    } else if (STREAM == 3 ||
+                               (STREAM == 4 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
+                                                uniform(max_nit_lane(nit)) < (uint32_t)U))) {
+                        static_assert(!WIRE || STREAM < 3, "wire mode uses the non-pipelined streams");
+                        if (fast) stream_tile_sorted_pl<U, true>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted_pl<U, false>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    } else if (STREAM == 1 ||
+                               (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
+                                                uniform(max_nit_lane(nit)) < (uint32_t)U))) {
+                        // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
+                        if (fast) stream_tile_sorted<U, true, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<U, false, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    } else {
+                        for (uint32_t s = 0; s < 16; ++s) {
+                            const uint32_t f = 4u * s + q;
+                            const FrameMeta6& fm = meta[f];  // broadcast read: one entry per 16-lane row
+                            const uint32_t f_lim = fm.lim;
+                            const uint32_t f_nit = (f_lim + 255u) >> 8;
+                            const uint32_t ns = max(max(rdlane(f_nit, 0), rdlane(f_nit, 16)),
+                                                    max(rdlane(f_nit, 32), rdlane(f_nit, 48)));
+                            if (ns == 0) continue;
+                            const uint32_t f_rowhi = fm.rowhi, f_packed = fm.packed;
+                            const uint32_t f_off = f_packed & 0xFFu, f_iphi = (f_packed >> 8) & 0xFFu;
+                            RowSums rs;
+                            if (fast) {
+                                ld.rel = fm.rel;
+                                stream_frame<U, WinLoader, WIRE, D2>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                            } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
+                                FarLoader fl;
+                                fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
+                                stream_frame<U, FarLoader, WIRE, D2>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                            }
+                            const uint32_t ric = row_sum_dpp(fold64(rs.ic));
+                            const uint32_t rip = row_sum_dpp(fold64(rs.ip));
+                            if (k == 15u) {
+                                sums_ic[f] = ric;
+                                sums_ip[f] = rip;
+                            }
                         }
                     }
                 }
-            }
 
-            // ---- 3. header phase (lane = frame); the window stays patched in LDS ---------------------
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (TRACE && threadIdx.x == 0 && i == 0) a.trace[1] = wall_clock64();  // frames streamed
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
-            const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
-            bool wb;
-            if (WIRE)
-                wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec[i],
-                                       &verd[i]);
-            else
-                wb = header_phase5<true, STREAM >= 1, D2>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, in_n, ok,
-                                                       parse, fi, cnt, &rec[i], &verd[i]);
-            wbm[i] = __ballot(wb);
+                // ---- 3. header phase (lane = frame); the window stays patched in LDS ---------------------
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (TRACE && threadIdx.x == 0 && i == 0) a.trace[1] = wall_clock64();  // frames streamed
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
+                const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
+                bool wb;
+                if (WIRE)
+                    wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
+                                           &verd_o);
+                else
+                    wb = header_phase5<true, STREAM >= 1, D2>(a, rows + lane * kWin, ip_raw, ic_raw, addr, len, in_n, ok,
+                                                           parse, fi, cnt, &rec_o, &verd_o);
+                wbm_o = __ballot(wb);
+                if (VT > 0 && i < VT) {  // keep the patched window in VGPRs; slot 0 streams the next tile
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_wave_barrier();
+                    const u32x4* rw = (const u32x4*)(rows + lane * kRowW);
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) vcur[c] = rw[c];
+                }
+            } while (0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();  // meta/sums are rewritten by the next tile
+            if constexpr (VT == 0) {
+                rec[i] = rec_o;
+                verd[i] = verd_o;
+                alo[i] = alo_o;
+                ahi[i] = ahi_o;
+                wbm[i] = wbm_o;
+            } else {
+#pragma unroll
+                for (int k = TPW - 1; k > 0; --k) {  // queue: tile i ends at index TPW - 1 - i
+                    rec[k] = rec[k - 1];
+                    verd[k] = verd[k - 1];
+                    alo[k] = alo[k - 1];
+                    ahi[k] = ahi[k - 1];
+                    wbm[k] = wbm[k - 1];
+                }
+                rec[0] = rec_o;
+                verd[0] = verd_o;
+                alo[0] = alo_o;
+                ahi[0] = ahi_o;
+                wbm[0] = wbm_o;
+                if (i < VT) {  // window queue: VGPR tile i ends at index VT - 1 - i
+#pragma unroll
+                    for (int k = (VT > 0 ? VT : 1) - 1; k > 0; --k)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) vwin[k][c] = vwin[k - 1][c];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) vwin[0][c] = vcur[c];
+                }
+            }
         }
 
         if (TRACE && threadIdx.x == 0) a.trace[2] = wall_clock64();  // header phase done
@@ -1257,15 +1311,17 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             if (lane == 0) atomicAdd(&s_arrive, 1u);
             if (uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
                 while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                       rounds_done * (uint32_t)kWaves6)
+                       rounds_done * (uint32_t)NW)
                     __builtin_amdgcn_s_sleep(2);
             }
         }
 #pragma unroll
-        for (int i = 0; i < TPW; ++i) {
+        for (int ii = 0; ii < TPW; ++ii) {
+            const int i = (ii + VT) % TPW;  // the LDS-slot tiles first, then the VGPR tiles (VT) through freed slots
+            const int qi = VT > 0 ? TPW - 1 - i : i;          // VT: tile i's outputs on the register queues
             uint32_t t = ub[i] + wave;
             if (NOWR) {  // keep the read phase alive without storing: fold the records into a counter
-                if (t < ue[i]) cnt.rxb += rec[i].x ^ rec[i].w ^ (uint32_t)wbm[i];
+                if (t < ue[i]) cnt.rxb += rec[qi].x ^ rec[qi].w ^ (uint32_t)wbm[qi];
                 continue;
             }
             if (t >= ue[i]) continue;
@@ -1273,15 +1329,24 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 t = front_tile(a, t);
                 if (t >= (a.n + kTile - 1) / kTile) continue;
             }
-            const uint8_t* rows = s_hdr[wave][i];
-            if (wbm[i]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
+            const uint8_t* rows = s_hdr[wave][i < VT ? i : i - VT];
+            if (i < VT && wbm[qi]) {  // a VGPR tile: its windows back into a slot whose stores have read it
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                u32x4* rw = (u32x4*)(s_hdr[wave][i < VT ? i : 0] + lane * kRowW);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) rw[c] = vwin[i < VT ? VT - 1 - i : 0][c];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (wbm[qi]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
                     const uint32_t kk = lane & 3u;
-                    const uint32_t flo = (uint32_t)__shfl((int)alo[i], (int)f, 64);
-                    const uint32_t fhi = (uint32_t)__shfl((int)ahi[i], (int)f, 64);
-                    if ((wbm[i] >> f) & 1ull) {
+                    const uint32_t flo = (uint32_t)__shfl((int)alo[qi], (int)f, 64);
+                    const uint32_t fhi = (uint32_t)__shfl((int)ahi[qi], (int)f, 64);
+                    if ((wbm[qi] >> f) & 1ull) {
                         const uint64_t fa = (uint64_t)flo | ((uint64_t)fhi << 32);
                         const u32x4 w = *(const u32x4*)(rows + f * kRowW + 16u * kk);
                         if (NTS) __builtin_nontemporal_store(w, (u32x4*)(a.umem + fa + 16u * kk));
@@ -1292,10 +1357,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
             if ((!SUBT || lane < a.tile_live) && fi < a.n) {
                 if (a.recs) {
-                    if (NTS) __builtin_nontemporal_store(rec[i], (u32x4*)a.recs + fi);
-                    else ((u32x4*)a.recs)[fi] = rec[i];
+                    if (NTS) __builtin_nontemporal_store(rec[qi], (u32x4*)a.recs + fi);
+                    else ((u32x4*)a.recs)[fi] = rec[qi];
                 }
-                if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[i];
+                if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[qi];
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1316,7 +1381,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     }
     if (DYN && threadIdx.x == 0) dq.leave();
     if (TRACE && threadIdx.x == 0) a.trace[3] = wall_clock64();  // write phase issued
-    store_partials<kWaves6>(a, cnt, s_cnt, wave, lane);
+    store_partials<NW>(a, cnt, s_cnt, wave, lane);
     if (TRACE && threadIdx.x == 0) a.trace[4] = wall_clock64();  // counters added
     if (WGT && threadIdx.x == 0 && a.partials) {
         a.partials[8192 + 2 * blockIdx.x] = wgt_start;
@@ -1388,6 +1453,24 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
     }
 }
 
+
+// The one-round kernel: 8 waves per workgroup (one workgroup per CU, 2 waves per SIMD, so up to 256 VGPRs
+// per lane), rounds of TPW tiles per wave of which the first VT keep their patched windows in VGPRs
+// (echo6_body VT) -- with TPW 8 / VT 4 a round is 64 tiles = 4096 frames per CU, a whole 1 M-frame batch's
+// share, so every byte is read before the first header sector is written, in ONE write phase at the end
+// (a write phase after every half share measured 24-26 us slower on c3's layout: wexp modes 62 / 65 / 66).
+constexpr int kWaves8 = 8;
+constexpr int kThreads8 = kWaves8 * 64;
+template <int U, int TPW, int VT, int SYNC = 0, int STREAM = 2, bool WGT = false, bool NOWR = false, bool MID = true,
+          bool D2 = true, bool SKM = true>
+__global__ __launch_bounds__(kThreads8, 1) void echo_kernel8(EchoArgs a, uint32_t tiles_per_wg) {
+    __shared__ Echo6Smem<TPW, false, STREAM, kWaves8, TPW - VT> sm;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t_begin = blockIdx.x * tiles_per_wg;
+    const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+    echo6_body<U, TPW, SYNC, STREAM, false, WGT, false, false, NOWR, MID, D2, SKM, false, false, false, false, kWaves8,
+               VT>(a, t_begin, t_end, tiles_per_wg, sm);
+}
 
 // Launch geometry: one workgroup per kWaves tiles (the dispatcher balances ragged tiles better than
 // a persistent grid: 315 vs 347 us at c3), capped so the partials workspace stays <= 512 KiB (the
