@@ -428,7 +428,7 @@ def test_timing_hook():
     assert cnt == 3 and ms > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96, 99, 101, 103, 104, 107, 108, 110, 111, 112, 113, 116, 117, 118])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96, 99, 101, 103, 104, 107, 108, 110, 111, 112, 113, 116, 117, 118, 119])
 @pytest.mark.parametrize("grid", [0, 1, 7])
 @pytest.mark.parametrize("len_hi", [2048, 112, 48])
 def test_kernel_variants_parity(variant, grid, len_hi):
@@ -460,6 +460,39 @@ def test_kernel_variants_parity(variant, grid, len_hi):
     assert (d_umem.cpu().numpy() == ref).all()
     if variant in (93, 95, 99, 101):  # dynamic schedules leave their queue counters zeroed for the next launch
         assert int(ws[768 << 10:(768 << 10) + 36].sum().item()) == 0
+
+
+@pytest.mark.parametrize("variant", [92, 119])
+@pytest.mark.parametrize("flen", [20, 33, 42, 63, 64, 100, 256, 300, 769, 1024, 1500, 4000, 9000])
+def test_uniform_tile_streams(variant, flen):
+    """Tiles whose frames all share one length and one 16-B offset (the uniform long-tile stream, ULONG: byte
+    masks computed once per tile) at several start offsets, plus a last partial tile and one odd frame out in
+    the middle tile (it falls back to the general streams) -- bit-exact against the oracle."""
+    L = X.tune_lib()
+    dev = _dev()
+    n = 64 * 5 + 17
+    stride = ((flen + 16 + 255) // 256) * 256 + 256
+    for off in (0, 1, 6, 15):
+        umem = np.zeros(n * stride + 256, np.uint8)
+        descs = oracle.synth_batch(umem, n, 256 + off, stride, seed=0x5EED1919 + flen + off, mode=0, len_lo=flen,
+                                   len_hi=flen)
+        descs["len"][64 * 2 + 5] = max(20, flen - 1)  # one frame of tile 2 ends elsewhere: general streams
+        ref = umem.copy()
+        v_ref, r_ref, _ = oracle.echo_batch(ref, descs)
+        d_umem, d_descs = to_dev(umem), to_dev(descs)
+        d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+        d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+        ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+        for grid in (0, 1):
+            rc = L.xsk_gpu__echo_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                         d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                         torch.cuda.current_stream().cuda_stream)
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert (d_verd.cpu().numpy() == v_ref).all(), (off, grid)
+            assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all(), (off, grid)
+            assert (d_umem.cpu().numpy() == ref).all(), (off, grid)
+            d_umem.copy_(to_dev(umem))
 
 
 def test_dynamic_schedule_full_size_and_reuse():

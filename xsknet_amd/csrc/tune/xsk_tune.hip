@@ -428,6 +428,10 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             // 117 / 118: 92 with software-pipelined ranked streams for every tile (STREAM 3) / ragged tiles (4)
             case 117: echo_kernel6<4, 2, 2, 3, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             case 118: echo_kernel6<4, 2, 2, 4, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 119: 92 with the uniform long-tile stream (ULONG: per-tile byte masks, no per-block mask logic);
+            // 120: 119 without the write phase
+            case 119: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 120: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, true><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

@@ -424,6 +424,7 @@ constexpr int kShip6Stream = 2;             // per-step streams for uniform long
 constexpr bool kShip6Mid = true;            // ping-size tiles (every frame within 128 B): 8 loads at once
 constexpr bool kShip6D2 = true;             // v_dot2_u32_u16 sums of halves (short, ping and per-step paths)
 constexpr bool kShip6Skm = true;            // ranked streams mask only slots where a frame ends
+constexpr bool kShip6Ulong = true;          // uniform long tiles: byte masks once per tile (stream_tile_uniform)
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -562,6 +563,48 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
     }
 }
 
+
+// Uniform long tiles (ULONG): every frame of the tile parsed, at the same 16-B offset and with the same end,
+// so the ICMP byte range [lo, hi) = [off + 34, off + len) is the same in every row.  A lane's byte masks are
+// then the same for every step: computed once per tile for the first and the last row-load (the only blocks
+// the range can cut; the others are whole or, past `lim`, not loaded), and a step costs its loads, one
+// v_dot2_u32_u16 per dword, two masks and the row reduction.  The sums are plain 32-bit sums of 16-bit halves
+// (< 2^32 for frames <= 64 KiB: 257 blocks x 8 halves x 65535 x 16 lanes); the IPv4 header sum comes from the
+// window in the header phase (IPH).
+template <int U>
+__device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
+                                                    uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
+                                                    uint32_t lane) {
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    const u32x4 mf = range_mask((int)(16u * k), (int)lo, (int)hi);                    // row-load 0
+    const u32x4 ml = range_mask((int)(256u * (ns - 1u) + 16u * k), (int)lo, (int)hi);  // row-load ns - 1
+    for (uint32_t s = 0; s < 16u; ++s) {
+        const uint32_t f = 4u * s + q;
+        const FrameMeta6& fm = meta[f];  // broadcast read: one entry per 16-lane row
+        const uint32_t rel = fm.rel, lim = fm.lim;
+        uint32_t h = 0;
+        for (uint32_t j0 = 0; j0 < ns; j0 += U) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ro < lim ? rel + ro : 0x80000000u), 0, kAuxNT);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t j = j0 + (uint32_t)u;  // wave-uniform
+                if (j >= ns) break;
+                u32x4 x = v[u];
+                if (j == 0u && k < 4u) *(u32x4*)(rows + f * kWin + 16u * k) = x;  // the 64-B header window
+                if (j == 0u) x &= mf;
+                if (j == ns - 1u) x &= ml;
+                h = sum_halves(x, h);
+            }
+        }
+        const uint32_t r = row_sum_dpp(h);
+        if (k == 15u) sums_ic[f] = r;
+    }
+}
 
 // stream_tile_sorted with the batches software-pipelined: batch b+1's U row-loads are issued before
 // batch b is consumed, so 1-2 batches stay in flight per lane instead of draining to zero at every
@@ -956,7 +999,7 @@ struct Echo6Smem {
 // echo_kernel8: 8 waves x 8 tiles = a whole 4096-frame CU share, written in ONE write phase at its end).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0>
+          bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, bool ULONG = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1206,6 +1249,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                         // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
                         if (fast) stream_tile_sorted<U, true, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                         else stream_tile_sorted<U, false, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                    } else if (ULONG && !WIRE && STREAM >= 1 && fast && __ballot(!parse) == 0ull &&
+                               __ballot(ukey != uniform(ukey)) == 0ull) {
+                        stream_tile_uniform<U>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
+                                               uniform(rowhi), lane);
                     } else {
                         for (uint32_t s = 0; s < 16; ++s) {
                             const uint32_t f = 4u * s + q;
@@ -1398,7 +1445,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // counter, zero on entry, left zero).  The static shares cover the rest (tiles_per_wg is recomputed).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, int TAIL = 0>
+          bool DYN = false, int TAIL = 0, bool ULONG = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1407,8 +1454,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         // wave-front order (a.front): every workgroup runs logical tiles [0, tiles_per_wg = 16 * passes)
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
-        echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN>(a, t_begin, t_end,
-                                                                                            tiles_per_wg, sm);
+        echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
+                   ULONG>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
