@@ -361,7 +361,7 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             args.front_mode = variant == 103 ? 1u : 2u;
             per = 16u * ((ntiles + front - 1) / front);
         }
-        if (variant == 90 || variant == 91) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
+        if (variant == 90 || variant == 91 || variant == 128 || variant == 129) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
             if (!d_workspace) return -EINVAL;
             HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
         }
@@ -430,8 +430,22 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 118: echo_kernel6<4, 2, 2, 4, false, false, false, false, false, true, true, true><<<gg, bb, 0, s>>>(args, per); break;
             // 119: 92 with the uniform long-tile stream (ULONG: per-tile byte masks, no per-block mask logic);
             // 120: 119 without the write phase
-            case 119: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, true><<<gg, bb, 0, s>>>(args, per); break;
-            case 120: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 119: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 120: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            // 121 / 122: the one-round kernel (112 / 108) with the uniform long-tile stream (ULONG)
+            case 121: echo_kernel8<6, 8, 4, 0, 2, false, false, true, true, true, 1><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            case 122: echo_kernel8<4, 8, 4, 0, 2, false, false, true, true, true, 1><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            // 123: 119 with the pipelined uniform stream (ULONG 2); 124: 123 without the write phase;
+            // 125: the one-round kernel (121) with it
+            case 123: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 124: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 125: echo_kernel8<4, 8, 4, 0, 2, false, false, true, true, true, 2><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
+            // 126: 119 with paired short tiles (PAIR); 127: 126 without the write phase
+            case 126: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 127: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, 1, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 128 / 129: 119 with a chip-wide barrier before (SYNC 3) / around (SYNC 4) every write phase
+            case 128: echo_kernel6<4, 2, 3, 2, false, false, false, false, false, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 129: echo_kernel6<4, 2, 4, 2, false, false, false, false, false, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

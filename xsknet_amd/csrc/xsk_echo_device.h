@@ -424,7 +424,8 @@ constexpr int kShip6Stream = 2;             // per-step streams for uniform long
 constexpr bool kShip6Mid = true;            // ping-size tiles (every frame within 128 B): 8 loads at once
 constexpr bool kShip6D2 = true;             // v_dot2_u32_u16 sums of halves (short, ping and per-step paths)
 constexpr bool kShip6Skm = true;            // ranked streams mask only slots where a frame ends
-constexpr bool kShip6Ulong = true;          // uniform long tiles: byte masks once per tile (stream_tile_uniform)
+constexpr int kShip6Ulong = 1;              // uniform long tiles: byte masks once per tile (stream_tile_uniform)
+constexpr bool kShip6Pair = true;           // both tiles of a round read at once when all frames fit their windows
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -603,6 +604,86 @@ __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc,
         }
         const uint32_t r = row_sum_dpp(h);
         if (k == 15u) sums_ic[f] = r;
+    }
+}
+
+// stream_tile_uniform with the row-loads software-pipelined (ULONG 2): the tile's 16 x ns row-loads per lane
+// form one sequence, issued in batches of U that may straddle steps, batch b + 1 issued before batch b is
+// summed, so a lane always has loads in flight while it sums (the per-step form drains to zero twice per
+// 1500-B step).  A step's frame (rel, lim) is read from the LDS metadata when its first row-load is issued;
+// its row sum is reduced and stored when its last row-load has been summed.
+struct UniCursor {
+    uint32_t s, j;     // next row-load to issue: step s, row-load j (wave-uniform)
+    uint32_t rel, lim; // the issuing step's frame (per 16-lane row)
+};
+template <int U>
+__device__ __forceinline__ void uni_issue(u32x4 (&v)[U], uint32_t (&tag)[U], UniCursor& c, uint32_t ns,
+                                          __amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint32_t q, uint32_t k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        tag[u] = 0xFFFFFFFFu;
+        v[u] = u32x4{0u, 0u, 0u, 0u};
+        if (c.s < 16u) {  // uniform
+            if (c.j == 0u) {
+                const FrameMeta6& fm = meta[4u * c.s + q];
+                c.rel = fm.rel;
+                c.lim = fm.lim;
+            }
+            const uint32_t ro = 256u * c.j + 16u * k;
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ro < c.lim ? c.rel + ro : 0x80000000u), 0, kAuxNT);
+            tag[u] = (c.s << 16) | c.j;
+            if (++c.j == ns) {
+                c.j = 0;
+                ++c.s;
+            }
+        }
+    }
+}
+template <int U>
+__device__ __forceinline__ void uni_consume(const u32x4 (&v)[U], const uint32_t (&tag)[U], uint32_t& h, uint32_t ns,
+                                            u32x4 mf, u32x4 ml, uint8_t* rows, uint32_t* sums_ic, uint32_t q,
+                                            uint32_t k) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if (tag[u] == 0xFFFFFFFFu) continue;  // uniform
+        const uint32_t s = tag[u] >> 16, j = tag[u] & 0xFFFFu, f = 4u * s + q;
+        u32x4 x = v[u];
+        if (j == 0u && k < 4u) *(u32x4*)(rows + f * kWin + 16u * k) = x;  // the 64-B header window
+        if (j == 0u) x &= mf;
+        if (j == ns - 1u) x &= ml;
+        h = sum_halves(x, h);
+        if (j == ns - 1u) {  // the step's frames are summed: reduce each row
+            const uint32_t r = row_sum_dpp(h);
+            if (k == 15u) sums_ic[f] = r;
+            h = 0;
+        }
+    }
+}
+template <int U>
+__device__ __forceinline__ void stream_tile_uniform_pl(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
+                                                       uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
+                                                       uint32_t lane) {
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    const u32x4 mf = range_mask((int)(16u * k), (int)lo, (int)hi);
+    const u32x4 ml = range_mask((int)(256u * (ns - 1u) + 16u * k), (int)lo, (int)hi);
+    UniCursor c{0u, 0u, 0u, 0u};
+    u32x4 A[U], B[U];
+    uint32_t ta[U], tb[U];
+    uint32_t h = 0;
+    uni_issue<U>(A, ta, c, ns, rsrc, meta, q, k);
+    for (;;) {  // ping-pong: issue the next batch, then sum the older one
+        if (c.s >= 16u) {
+            uni_consume<U>(A, ta, h, ns, mf, ml, rows, sums_ic, q, k);
+            break;
+        }
+        uni_issue<U>(B, tb, c, ns, rsrc, meta, q, k);
+        uni_consume<U>(A, ta, h, ns, mf, ml, rows, sums_ic, q, k);
+        if (c.s >= 16u) {
+            uni_consume<U>(B, tb, h, ns, mf, ml, rows, sums_ic, q, k);
+            break;
+        }
+        uni_issue<U>(A, ta, c, ns, rsrc, meta, q, k);
+        uni_consume<U>(B, tb, h, ns, mf, ml, rows, sums_ic, q, k);
     }
 }
 
@@ -993,13 +1074,119 @@ struct Echo6Smem {
 // workgroup calls it with the same range): rounds of kWaves6 * TPW tiles, read phase, write phase, and
 // the counters (store_partials).  echo_kernel6 runs it once per workgroup on its static share; the
 // low-latency persistent kernel (xsk_lowlat.hip) once per doorbell.
+// One frame's descriptor checks and stream geometry (reference mode), as the round body computes them.
+struct FrameIn {
+    uint64_t addr, a16;
+    uint32_t len, off, rowhi, lim;
+    bool ok, parse;
+};
+__device__ __forceinline__ FrameIn frame_in(const EchoArgs& a, u32x4 dsc, bool in_n) {
+    FrameIn F;
+    F.addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
+    F.len = dsc.z;
+    const uint64_t need = F.len >= 20 ? (F.len > 38 ? F.len : 38) : F.len;  // xsk_receive.c:120-157
+    F.ok = in_n && F.len <= kMaxLen && F.addr <= a.umem_size && need <= a.umem_size - F.addr;
+    F.parse = F.ok && F.len >= 20u;
+    F.a16 = F.addr & ~15ull;
+    F.off = (uint32_t)F.addr & 15u;
+    F.rowhi = F.parse ? F.off + F.len : 0u;
+    const uint32_t wend = F.ok ? (uint32_t)min(a.umem_size - F.a16, (uint64_t)kWin) : 0u;
+    F.lim = max(F.rowhi, F.parse ? wend : 0u);
+    return F;
+}
+
+// PAIR: both tiles of a wave's round read at once when every frame of both fits its 64-B window (c2:
+// minimum-size frames).  The two descriptor loads go out together, then all eight 16-B frame loads of the
+// two tiles (4 lanes per frame, 16 frames per wave-load; a frame's address and limit come from its owner
+// lane by bpermute, so neither tile needs the LDS metadata), and only then are they summed -- the round
+// pays two memory round trips instead of four, with twice the bytes in flight.  The windows go to the two
+// LDS slots, the ICMP sums to the two sum rows (the IPv4 header sum comes from the window: IPH), then the
+// header phase of each tile.  Returns false (nothing written) when either tile has a longer frame.
+template <bool SYNC2>
+__device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0, uint32_t t1, uint8_t* rows0,
+                                                  uint8_t* rows1, uint32_t* sums0, uint32_t* sums1, uint32_t lane,
+                                                  Counters& cnt, u32x4* rec, uint32_t* verd, uint32_t* alo,
+                                                  uint32_t* ahi, uint64_t* wbm, uint32_t& round_long) {
+    if (a.front) return false;
+    const uint32_t fi0 = t0 * kTile + lane, fi1 = t1 * kTile + lane;
+    const bool in0 = fi0 < a.n, in1 = fi1 < a.n;
+    u32x4 d0 = u32x4{0u, 0u, 0u, 0u}, d1 = u32x4{0u, 0u, 0u, 0u};
+    if (in0) d0 = *(const u32x4*)(a.descs + fi0);
+    if (in1) d1 = *(const u32x4*)(a.descs + fi1);
+    const FrameIn F0 = frame_in(a, d0, in0), F1 = frame_in(a, d1, in1);
+    if ((__ballot(F0.lim > (uint32_t)kWin) | __ballot(F1.lim > (uint32_t)kWin)) != 0ull) return false;
+    const uint32_t kk = lane & 3u, ro = 16u * kk;
+    u32x4 x0[4], x1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int src = r * 16 + (int)(lane >> 2);
+        const uint64_t b0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(F0.a16 >> 32), src, 64) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)F0.a16, src, 64);
+        const uint64_t b1 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(F1.a16 >> 32), src, 64) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)F1.a16, src, 64);
+        const uint32_t m0 = (uint32_t)__shfl((int)F0.lim, src, 64), m1 = (uint32_t)__shfl((int)F1.lim, src, 64);
+        x0[r] = u32x4{0u, 0u, 0u, 0u};
+        x1[r] = u32x4{0u, 0u, 0u, 0u};
+        if (ro < m0) x0[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + b0 + ro));
+        if (ro < m1) x1[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + b1 + ro));
+    }
+    // the ICMP bytes [off + 34, rowhi): masks once per tile when every frame has the same offset and end
+    const uint32_t k0 = (F0.off << 24) ^ F0.rowhi, k1 = (F1.off << 24) ^ F1.rowhi;
+    const bool u0 = __ballot(k0 != uniform(k0)) == 0ull, u1 = __ballot(k1 != uniform(k1)) == 0ull;
+    const u32x4 mk0 = range_mask((int)ro, (int)uniform(F0.off) + 34, (int)uniform(F0.rowhi));
+    const u32x4 mk1 = range_mask((int)ro, (int)uniform(F1.off) + 34, (int)uniform(F1.rowhi));
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const FrameIn& F = tt ? F1 : F0;
+        uint8_t* rows = tt ? rows1 : rows0;
+        uint32_t* sums = tt ? sums1 : sums0;
+        const bool uni = tt ? u1 : u0;
+        const u32x4 mk = tt ? mk1 : mk0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+            const u32x4 v = tt ? x1[r] : x0[r];
+            *(u32x4*)(rows + f * kWin + ro) = v;
+            uint32_t ric;
+            if (uni) {
+                ric = sum_halves(v & mk, 0u);
+            } else {
+                const int fo = __shfl((int)F.off, (int)f, 64), fh = __shfl((int)F.rowhi, (int)f, 64);
+                ric = sum_range_h(v, (int)ro, fo + 34, fh);
+            }
+            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0xB1, 0xF, 0xF, false);  // xor 1
+            ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);  // xor 2
+            if (kk == 0u) sums[f] = ric;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    bool wb = header_phase5<true, true, true>(a, rows0 + lane * kWin, 0u, sums0[lane], F0.addr, F0.len, in0, F0.ok,
+                                             F0.parse, fi0, cnt, &rec[0], &verd[0]);
+    wbm[0] = __ballot(wb);
+    wb = header_phase5<true, true, true>(a, rows1 + lane * kWin, 0u, sums1[lane], F1.addr, F1.len, in1, F1.ok,
+                                        F1.parse, fi1, cnt, &rec[1], &verd[1]);
+    wbm[1] = __ballot(wb);
+    alo[0] = d0.x;
+    ahi[0] = d0.y;
+    alo[1] = d1.x;
+    ahi[1] = d1.y;
+    if (SYNC2)
+        round_long += (uint32_t)__popcll(__ballot(in0 && F0.len >= kHeavyLen)) +
+                      (uint32_t)__popcll(__ballot(in1 && F1.len >= kHeavyLen));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // the sums / windows are rewritten by the next round
+    return true;
+}
+
 // NW: waves per workgroup.  VT: the first VT tiles of a wave's round keep their patched header windows in
 // VGPRs (lane = frame, 64 B) instead of an LDS slot -- they stream through slot 0 and are copied out after
 // their header phase -- so a round holds TPW tiles per wave in TPW - VT LDS slots (the one-round kernel,
 // echo_kernel8: 8 waves x 8 tiles = a whole 4096-frame CU share, written in ONE write phase at its end).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, bool ULONG = false>
+          bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
+          bool PAIR = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1069,9 +1256,17 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         // VT == 0: the TPW slots unrolled, every tile's outputs straight into the per-slot arrays; VT > 0 (8
         // tiles per wave): a rolled loop whose outputs are pushed onto register queues with constant indices
         // (dynamically indexed VGPR arrays would live in scratch memory)
+        static_assert(!PAIR || (TPW == 2 && !WIRE && !SUBT && !PF && !DYN && VT == 0 && D2 && STREAM >= 1),
+                      "paired short tiles: two-tile rounds in reference mode with dot2 sums and IPH");
+        bool paired = false;
+        if (PAIR && ub[0] + wave < ue[0] && ub[1] + wave < ue[1])  // wave-uniform
+            paired = read_round_short2<SYNC == 2>(a, ub[0] + wave, ub[1] + wave, s_hdr[wave][0], s_hdr[wave][TPW > 1 ? 1 : 0],
+                                                  sm.sum[wave][0], sm.sum[wave][1], lane, cnt, rec, verd, alo, ahi,
+                                                  wbm, round_long);
         constexpr int kReadUnroll = VT > 0 ? 1 : TPW;
 #pragma unroll kReadUnroll
         for (int i = 0; i < TPW; ++i) {
+            if (PAIR && paired) continue;  // wave-uniform: both tiles are done
             const uint32_t ub_i = VT > 0 ? ub[0] + (uint32_t)i * NW : ub[i], ue_i = VT > 0 ? ue[0] : ue[i];
             u32x4 rec_o;
             uint32_t verd_o, alo_o, ahi_o;
@@ -1251,8 +1446,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                         else stream_tile_sorted<U, false, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                     } else if (ULONG && !WIRE && STREAM >= 1 && fast && __ballot(!parse) == 0ull &&
                                __ballot(ukey != uniform(ukey)) == 0ull) {
-                        stream_tile_uniform<U>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
-                                               uniform(rowhi), lane);
+                        if (ULONG == 2)
+                            stream_tile_uniform_pl<U>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
+                                                      uniform(rowhi), lane);
+                        else
+                            stream_tile_uniform<U>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
+                                                   uniform(rowhi), lane);
                     } else {
                         for (uint32_t s = 0; s < 16; ++s) {
                             const uint32_t f = 4u * s + q;
@@ -1445,7 +1644,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // counter, zero on entry, left zero).  The static shares cover the rest (tiles_per_wg is recomputed).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, int TAIL = 0, bool ULONG = false>
+          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1455,7 +1654,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
@@ -1509,14 +1708,14 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
 constexpr int kWaves8 = 8;
 constexpr int kThreads8 = kWaves8 * 64;
 template <int U, int TPW, int VT, int SYNC = 0, int STREAM = 2, bool WGT = false, bool NOWR = false, bool MID = true,
-          bool D2 = true, bool SKM = true>
+          bool D2 = true, bool SKM = true, int ULONG = 0>
 __global__ __launch_bounds__(kThreads8, 1) void echo_kernel8(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, false, STREAM, kWaves8, TPW - VT> sm;
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
     echo6_body<U, TPW, SYNC, STREAM, false, WGT, false, false, NOWR, MID, D2, SKM, false, false, false, false, kWaves8,
-               VT>(a, t_begin, t_end, tiles_per_wg, sm);
+               VT, ULONG>(a, t_begin, t_end, tiles_per_wg, sm);
 }
 
 // Launch geometry: one workgroup per kWaves tiles (the dispatcher balances ragged tiles better than
