@@ -540,7 +540,8 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
             const u32x4 x = v[u];
             if (uj[u] == 0u) {
                 if (k < kRowW / 16u && ulim[u]) *(u32x4*)(rows + uf[u] * kRowW + ro) = x;  // the header window
-                ic += sum_range(x, (int)ro, WIRE ? 128 : (int)uoff[u] + 34, (int)urowhi[u]);
+                if (D2) h += sum_range_h(x, (int)ro, WIRE ? 128 : (int)uoff[u] + 34, (int)urowhi[u]);
+                else ic += sum_range(x, (int)ro, WIRE ? 128 : (int)uoff[u] + 34, (int)urowhi[u]);
             } else {
                 const int nb = (int)(urowhi[u] - min(ro, urowhi[u]));
                 u32x4 y = x;
@@ -1186,7 +1187,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false>
+          bool PAIR = false, bool RD2 = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1442,8 +1443,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                                (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                                 uniform(max_nit_lane(nit)) < (uint32_t)U))) {
                         // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
-                        if (fast) stream_tile_sorted<U, true, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                        else stream_tile_sorted<U, false, WIRE, false, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                        if (fast) stream_tile_sorted<U, true, WIRE, RD2 && !WIRE, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<U, false, WIRE, RD2 && !WIRE, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                     } else if (ULONG && !WIRE && STREAM >= 1 && fast && __ballot(!parse) == 0ull &&
                                __ballot(ukey != uniform(ukey)) == 0ull) {
                         if (ULONG == 2)
@@ -1644,7 +1645,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // counter, zero on entry, left zero).  The static shares cover the rest (tiles_per_wg is recomputed).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false>
+          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1654,7 +1655,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
