@@ -197,8 +197,8 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
         echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2, kShip6Skm,
                      true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (!small)  // wire mode: 128-B windows, one tile per wave per round
-        echo_kernel6<kShip6U, 1, kShip6Sync, kShip6Stream, false, false, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(
-            args, tiles_per_wg);
+        echo_kernel6<kShip6U, 1, kShip6Sync, kShip6Stream, false, false, true, false, false, false, false, false, false,
+                     false, 0, kShip6Ulong><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else
         echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, true, false, false, false, false, false, true>
             <<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);

@@ -573,10 +573,13 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
 // v_dot2_u32_u16 per dword, two masks and the row reduction.  The sums are plain 32-bit sums of 16-bit halves
 // (< 2^32 for frames <= 64 KiB: 257 blocks x 8 halves x 65535 x 16 lanes); the IPv4 header sum comes from the
 // window in the header phase (IPH).
-template <int U>
+// WIRE (wire-format mode): 128-B windows, and the stream sums row bytes [128, rowhi) (lo = 128): the header
+// phase completes the message sum from the window once it has parsed the headers.
+template <int U, bool WIRE = false>
 __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
                                                     uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
                                                     uint32_t lane) {
+    constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;
     const uint32_t q = lane >> 4, k = lane & 15u;
     const u32x4 mf = range_mask((int)(16u * k), (int)lo, (int)hi);                    // row-load 0
     const u32x4 ml = range_mask((int)(256u * (ns - 1u) + 16u * k), (int)lo, (int)hi);  // row-load ns - 1
@@ -597,7 +600,7 @@ __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc,
                 const uint32_t j = j0 + (uint32_t)u;  // wave-uniform
                 if (j >= ns) break;
                 u32x4 x = v[u];
-                if (j == 0u && k < 4u) *(u32x4*)(rows + f * kWin + 16u * k) = x;  // the 64-B header window
+                if (j == 0u && k < kRowW / 16u) *(u32x4*)(rows + f * kRowW + 16u * k) = x;  // the header window
                 if (j == 0u) x &= mf;
                 if (j == ns - 1u) x &= ml;
                 h = sum_halves(x, h);
@@ -1187,7 +1190,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1225,6 +1228,15 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     const uint32_t r_end = SYNC >= 3 ? t_begin + tiles_per_wg : t_end;
     DynQueue dq;
     if (DYN && threadIdx.x == 0) dq.init(a, TPW);
+    // CARRY: the last tile of a round that is not the workgroup's last keeps its patched windows, record and
+    // verdict in VGPRs and is written in the NEXT round's write phase, so a two-round share (c3) writes a
+    // quarter of its header sectors in mid-kernel instead of half (writes that meet the other workgroups'
+    // reads cost about twice as much as the ones at the end: wexp modes 62 / 65)
+    static_assert(!CARRY || (!DYN && VT == 0 && !SUBT && !WIRE && SYNC < 3), "carry: static shares, reference mode");
+    u32x4 cwin[4], crec = u32x4{0u, 0u, 0u, 0u};
+    uint32_t cverd = 0, calo = 0, cahi = 0, cfi = 0;
+    uint64_t cwbm = 0;
+    bool carried = false;  // wave-uniform
     uint32_t r0 = t_begin;
     for (;;) {  // rounds, workgroup-uniform
         // slot i of this round: wave w streams tile ub[i] + w when it is below ue[i]
@@ -1248,6 +1260,14 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             }
             r0 += kRound;
         }
+        // CARRY: the tile carried out of the previous round is written in this round's write phase
+        const bool carried_prev = CARRY && carried;
+        u32x4 pwin[4], prec = crec;
+        const uint32_t pverd = cverd, palo = calo, pahi = cahi, pfi = cfi;
+        const uint64_t pwbm = cwbm;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pwin[c] = cwin[c];
+        carried = false;
         u32x4 rec[TPW];
         u32x4 vwin[VT > 0 ? VT : 1][4];  // VT: patched windows of the VGPR tiles (lane = frame, 64 B)
         uint32_t verd[TPW], alo[TPW], ahi[TPW];
@@ -1445,14 +1465,14 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                         // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
                         if (fast) stream_tile_sorted<U, true, WIRE, RD2 && !WIRE, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                         else stream_tile_sorted<U, false, WIRE, RD2 && !WIRE, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
-                    } else if (ULONG && !WIRE && STREAM >= 1 && fast && __ballot(!parse) == 0ull &&
+                    } else if (ULONG && (WIRE || STREAM >= 1) && fast && __ballot(!parse) == 0ull &&
                                __ballot(ukey != uniform(ukey)) == 0ull) {
-                        if (ULONG == 2)
+                        if (ULONG == 2 && !WIRE)
                             stream_tile_uniform_pl<U>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
                                                       uniform(rowhi), lane);
                         else
-                            stream_tile_uniform<U>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
-                                                   uniform(rowhi), lane);
+                            stream_tile_uniform<U, WIRE>(ld.r, meta, rows, sums_ic, uniform(nit),
+                                                         WIRE ? 128u : uniform(off) + 34u, uniform(rowhi), lane);
                     } else {
                         for (uint32_t s = 0; s < 16; ++s) {
                             const uint32_t f = 4u * s + q;
@@ -1577,6 +1597,21 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 if (t >= (a.n + kTile - 1) / kTile) continue;
             }
             const uint8_t* rows = s_hdr[wave][i < VT ? i : i - VT];
+            if (CARRY && i == TPW - 1 && r0 < r_end) {  // not the last round: keep this tile for the next one
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                const u32x4* rw = (const u32x4*)(rows + lane * kRowW);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) cwin[c] = rw[c];
+                crec = rec[qi];
+                cverd = verd[qi];
+                calo = alo[qi];
+                cahi = ahi[qi];
+                cwbm = wbm[qi];
+                cfi = t * (uint32_t)kTile + lane;
+                carried = true;
+                continue;
+            }
             if (i < VT && wbm[qi]) {  // a VGPR tile: its windows back into a slot whose stores have read it
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_wave_barrier();
@@ -1608,6 +1643,32 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     else ((u32x4*)a.recs)[fi] = rec[qi];
                 }
                 if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[qi];
+            }
+        }
+        if (CARRY && carried_prev) {  // the previous round's carried tile, through slot 0 (its stores have read it)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            u32x4* rw = (u32x4*)(s_hdr[wave][0] + lane * kRowW);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) rw[c] = pwin[c];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (pwbm) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                    const uint32_t kk = lane & 3u;
+                    const uint32_t flo = (uint32_t)__shfl((int)palo, (int)f, 64);
+                    const uint32_t fhi = (uint32_t)__shfl((int)pahi, (int)f, 64);
+                    if ((pwbm >> f) & 1ull) {
+                        const uint64_t fa = (uint64_t)flo | ((uint64_t)fhi << 32);
+                        *(u32x4*)(a.umem + fa + 16u * kk) = *(const u32x4*)(s_hdr[wave][0] + f * kRowW + 16u * kk);
+                    }
+                }
+            }
+            if (pfi < a.n) {
+                if (a.recs) ((u32x4*)a.recs)[pfi] = prec;
+                if (a.verdicts) a.verdicts[pfi] = (uint8_t)pverd;
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1645,7 +1706,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // counter, zero on entry, left zero).  The static shares cover the rest (tiles_per_wg is recomputed).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false>
+          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1655,7 +1716,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR, RD2>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2, CARRY>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
