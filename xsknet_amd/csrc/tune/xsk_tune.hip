@@ -361,6 +361,8 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             args.front_mode = variant == 103 ? 1u : 2u;
             per = 16u * ((ntiles + front - 1) / front);
         }
+        if (variant == 134 || variant == 136) args.rot = 37;  // 131 with rotated shares
+        if (variant == 135 || variant == 136) args.srot = 5;  // 131 with rotated uniform-stream steps
         if (variant == 90 || variant == 91 || variant == 128 || variant == 129) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
             if (!d_workspace) return -EINVAL;
             HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
@@ -453,6 +455,13 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 132: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, true><<<gg, bb, 0, s>>>(args, per); break;
             // 133: shipped + the cross-round carry of each round's last tile (CARRY)
             case 133: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 134: shipped with rotated shares (EchoArgs::rot); 135: with rotated uniform-stream steps (srot); 136: both
+            case 134:
+            case 135:
+            case 136: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 137 / 138: shipped + the penultimate round's windows deferred to the end (DEFW 1: heavy waves; 2: all)
+            case 137: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 138: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

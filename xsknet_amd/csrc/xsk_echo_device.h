@@ -53,12 +53,28 @@ struct EchoArgs {
     // 16 g + w of a pass; 2: tile w * grid + g.  Each workgroup then runs logical tiles [0, 16 * passes).
     uint32_t front = 0;
     uint32_t front_mode = 1;
+    // round kernel, static shares only (tuning): nonzero = ROTATED shares.  Workgroup g starts its share of
+    // L tiles at logical tile (g * rot) mod L and wraps, so the workgroups that run in step are not all at
+    // the same offset of their (power-of-two aligned) shares at the same time.
+    uint32_t rot = 0;
+    // uniform long-tile stream only (tuning): nonzero = the 16 steps of a tile start at step
+    // (wave * srot + blockIdx.x) mod 16 instead of 0, so the waves of the chip do not stream the same
+    // frame slots of their tiles at the same time
+    uint32_t srot = 0;
 };
 
 // Physical tile of logical tile lt (lt & 15 = the wave, lt >> 4 = the pass) in the wave-front order.
 __device__ __forceinline__ uint32_t front_tile(const EchoArgs& a, uint32_t lt) {
     const uint32_t pass = lt >> 4, w = lt & 15u;
     return pass * a.front + (a.front_mode == 2 ? w * gridDim.x + blockIdx.x : blockIdx.x * 16u + w);
+}
+
+// Physical tile of logical tile t of the share [tb, te) in the rotated order (a.rot != 0).
+__device__ __forceinline__ uint32_t rot_tile(const EchoArgs& a, uint32_t t, uint32_t tb, uint32_t te) {
+    const uint32_t L = te - tb;
+    uint32_t x = t - tb + (blockIdx.x * a.rot) % L;
+    x = x >= L ? x - L : x;
+    return tb + x;
 }
 
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
@@ -403,6 +419,26 @@ __device__ __forceinline__ bool header_phase5(const EchoArgs& a, uint8_t* row, u
     return wb;
 }
 
+// The echo-reply rewrite of a 16-B aligned frame's 64-B window in place (header_phase5's `wb` branch, from the
+// window's own bytes): for a frame already known to be a TX_REPLY whose window is written back whole.
+__device__ __forceinline__ void repatch_window(uint8_t* row) {
+    uint32_t* r32 = (uint32_t*)row;
+    uint32_t h[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h[k] = r32[k];
+    const uint32_t csum_le = h[9] & 0xFFFFu;
+    uint32_t c16 = (~csum_le) & 0xFFFFu;
+    c16 = (c16 + 0xFFF7u) & 0xFFFFu;
+    c16 += c16 < 0xFFF7u ? 1u : 0u;
+    r32[0] = (h[1] >> 16) | (h[2] << 16);
+    r32[1] = (h[2] >> 16) | (h[0] << 16);
+    r32[2] = (h[0] >> 16) | (h[1] << 16);
+    r32[6] = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);
+    r32[7] = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);
+    r32[8] = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);
+    r32[9] = (h[9] & 0xFFFF0000u) | ((~c16) & 0xFFFFu);
+}
+
 // ================================================================================================
 // The round kernel (shipped).  Measured on cold 4 GiB slabs (tools/wexp.hip): a read stream that
 // meets scattered 64-B writes pays for them at DRAM read/write turnarounds (+61 us for 1 M header
@@ -578,13 +614,13 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
 template <int U, bool WIRE = false>
 __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
                                                     uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
-                                                    uint32_t lane) {
+                                                    uint32_t lane, uint32_t s0 = 0) {
     constexpr uint32_t kRowW = WIRE ? 128u : (uint32_t)kWin;
     const uint32_t q = lane >> 4, k = lane & 15u;
     const u32x4 mf = range_mask((int)(16u * k), (int)lo, (int)hi);                    // row-load 0
     const u32x4 ml = range_mask((int)(256u * (ns - 1u) + 16u * k), (int)lo, (int)hi);  // row-load ns - 1
     for (uint32_t s = 0; s < 16u; ++s) {
-        const uint32_t f = 4u * s + q;
+        const uint32_t f = 4u * ((s + s0) & 15u) + q;
         const FrameMeta6& fm = meta[f];  // broadcast read: one entry per 16-lane row
         const uint32_t rel = fm.rel, lim = fm.lim;
         uint32_t h = 0;
@@ -1190,7 +1226,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false, bool CARRY = false>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1237,6 +1273,14 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     uint32_t cverd = 0, calo = 0, cahi = 0, cfi = 0;
     uint64_t cwbm = 0;
     bool carried = false;  // wave-uniform
+    // DEFW: the windows of the penultimate round of the share are not written in its write phase but re-read,
+    // re-patched and written after the last round's, so a two-round share (c3) has no write phase in mid-kernel
+    // (wexp: one write phase at the end of a share 250 us, one after each half 275 us).  DEFW 1: only waves
+    // whose round was heavy (SYNC 2's test) defer; 2: every wave.  Records and verdicts are written as usual.
+    static_assert(!DEFW || (!DYN && VT == 0 && !SUBT && !WIRE && SYNC < 3 && !CARRY), "deferred windows: static shares, reference mode");
+    uint64_t dwbm[TPW];
+    uint32_t dalo[TPW], dahi[TPW];
+    bool have_def = false;  // wave-uniform
     uint32_t r0 = t_begin;
     for (;;) {  // rounds, workgroup-uniform
         // slot i of this round: wave w streams tile ub[i] + w when it is below ue[i]
@@ -1281,7 +1325,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                       "paired short tiles: two-tile rounds in reference mode with dot2 sums and IPH");
         bool paired = false;
         if (PAIR && ub[0] + wave < ue[0] && ub[1] + wave < ue[1])  // wave-uniform
-            paired = read_round_short2<SYNC == 2>(a, ub[0] + wave, ub[1] + wave, s_hdr[wave][0], s_hdr[wave][TPW > 1 ? 1 : 0],
+            paired = read_round_short2<SYNC == 2>(a, (!SUBT && !DYN && a.rot) ? rot_tile(a, ub[0] + wave, t_begin, t_end) : ub[0] + wave,
+                                                  (!SUBT && !DYN && a.rot) ? rot_tile(a, ub[1] + wave, t_begin, t_end) : ub[1] + wave, s_hdr[wave][0], s_hdr[wave][TPW > 1 ? 1 : 0],
                                                   sm.sum[wave][0], sm.sum[wave][1], lane, cnt, rec, verd, alo, ahi,
                                                   wbm, round_long);
         constexpr int kReadUnroll = VT > 0 ? 1 : TPW;
@@ -1305,6 +1350,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     t = front_tile(a, t);
                     if (t >= (a.n + kTile - 1) / kTile) break;
                 }
+                if (!SUBT && !DYN && a.rot) t = rot_tile(a, t, t_begin, t_end);
                 asm volatile("" : "+v"(lane));
                 uint8_t* rows = s_hdr[wave][i < VT ? 0 : i - VT];  // VGPR tiles pass through slot 0
                 const uint32_t q = lane >> 4, k = lane & 15u;
@@ -1472,7 +1518,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                                                       uniform(rowhi), lane);
                         else
                             stream_tile_uniform<U, WIRE>(ld.r, meta, rows, sums_ic, uniform(nit),
-                                                         WIRE ? 128u : uniform(off) + 34u, uniform(rowhi), lane);
+                                                         WIRE ? 128u : uniform(off) + 34u, uniform(rowhi), lane,
+                                                         a.srot ? (wave * a.srot + blockIdx.x) & 15u : 0u);
                     } else {
                         for (uint32_t s = 0; s < 16; ++s) {
                             const uint32_t f = 4u * s + q;
@@ -1582,6 +1629,14 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     __builtin_amdgcn_s_sleep(2);
             }
         }
+        // DEFW: this round is the penultimate one of the share (the next is the last): keep its windows
+        const bool defer = DEFW && !DYN && r0 < r_end && r0 + kRound >= r_end &&
+                           (DEFW == 2 || uniform(round_long) * 2u >= (uint32_t)(kTile * TPW));
+        if (defer) {
+            have_def = true;
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) dwbm[i] = 0ull;
+        }
 #pragma unroll
         for (int ii = 0; ii < TPW; ++ii) {
             const int i = (ii + VT) % TPW;  // the LDS-slot tiles first, then the VGPR tiles (VT) through freed slots
@@ -1596,6 +1651,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 t = front_tile(a, t);
                 if (t >= (a.n + kTile - 1) / kTile) continue;
             }
+            if (!SUBT && !DYN && a.rot) t = rot_tile(a, t, t_begin, t_end);
             const uint8_t* rows = s_hdr[wave][i < VT ? i : i - VT];
             if (CARRY && i == TPW - 1 && r0 < r_end) {  // not the last round: keep this tile for the next one
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1621,7 +1677,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_wave_barrier();
             }
-            if (wbm[qi]) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
+            if (DEFW && defer) {
+                dwbm[i] = wbm[qi];
+                dalo[i] = alo[qi];
+                dahi[i] = ahi[qi];
+            }
+            if (wbm[qi] && !(DEFW && defer)) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
@@ -1687,6 +1748,45 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             __syncthreads();
         }
     }
+    if (DEFW && have_def) {  // the deferred windows: re-read (unchanged since), re-patched, written
+        u32x4 x[TPW][4];
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t f = (uint32_t)r * 16u + (lane >> 2), kk = lane & 3u;
+                const uint64_t fa = (uint64_t)(uint32_t)__shfl((int)dalo[i], (int)f, 64) |
+                                    ((uint64_t)(uint32_t)__shfl((int)dahi[i], (int)f, 64) << 32);
+                x[i][r] = u32x4{0u, 0u, 0u, 0u};
+                if ((dwbm[i] >> f) & 1ull) x[i][r] = __builtin_nontemporal_load((const u32x4*)(a.umem + fa + 16u * kk));
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t f = (uint32_t)r * 16u + (lane >> 2), kk = lane & 3u;
+                *(u32x4*)(s_hdr[wave][i] + f * kWin + 16u * kk) = x[i][r];
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+            if ((dwbm[i] >> lane) & 1ull) repatch_window(s_hdr[wave][i] + lane * kWin);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t f = (uint32_t)r * 16u + (lane >> 2), kk = lane & 3u;
+                const uint64_t fa = (uint64_t)(uint32_t)__shfl((int)dalo[i], (int)f, 64) |
+                                    ((uint64_t)(uint32_t)__shfl((int)dahi[i], (int)f, 64) << 32);
+                if ((dwbm[i] >> f) & 1ull)
+                    *(u32x4*)(a.umem + fa + 16u * kk) = *(const u32x4*)(s_hdr[wave][i] + f * kWin + 16u * kk);
+            }
+    }
     if (DYN && threadIdx.x == 0) dq.leave();
     if (TRACE && threadIdx.x == 0) a.trace[3] = wall_clock64();  // write phase issued
     store_partials<NW>(a, cnt, s_cnt, wave, lane);
@@ -1706,7 +1806,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // counter, zero on entry, left zero).  The static shares cover the rest (tiles_per_wg is recomputed).
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
-          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false>
+          bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false,
+          int DEFW = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1716,7 +1817,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR, RD2, CARRY>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2, CARRY, DEFW>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
