@@ -1,0 +1,94 @@
+"""In-process cold A/B of kernel variants (tuning aid, not the bench).
+
+Box-to-box and process-to-process drift (±3 % on c3) hides differences of a few microseconds between
+separate `bench.py --variant` runs.  This tool times several variants inside ONE process on ONE pool of
+never-touched batches: in round r, batch b runs variant V[(b + r) % len(V)], so every variant sees every
+pool position; each launch is bracketed by its own pair of HIP events on the launch stream.  Between rounds
+the pool is regenerated (untimed), so diagnostic variants with wrong results cannot poison the next round.
+Variant -1 is the shipped entry point (xsk_gpu_echo_dev).
+
+    python tools/abbench.py --config c3 --variants=-1,131,139 --rounds 3
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import CONFIGS  # noqa: E402
+import xsknet_amd as X  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--variants", default="-1,131")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--pool", type=int, default=0, help="batches in the pool (0: as many as fit, <= 24)")
+    args = ap.parse_args()
+    V = [int(v) for v in args.variants.split(",")]
+    dev = torch.device("cuda", 0)
+    n, lo, hi, stride, seed, desc = CONFIGS[args.config]
+    bb = n * stride
+    free, _ = torch.cuda.mem_get_info(dev)
+    pool = args.pool or max(len(V), min(24, int(free * 0.8) // (bb + n * 16) - 1))
+    pool -= pool % len(V)
+    slab = torch.empty(pool * bb, dtype=torch.uint8, device=dev)
+    descs = [torch.empty(n * 16, dtype=torch.uint8, device=dev) for _ in range(pool)]
+    verd = torch.empty(n, dtype=torch.uint8, device=dev)
+    recs = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    stats = torch.zeros(40, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(max(1 << 20, X.workspace_size(0, n)), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    tune = X.tune_lib() if any(v >= 0 for v in V) else None
+
+    def regen():
+        for b in range(pool):
+            X.synth_dev(slab[b * bb:(b + 1) * bb], descs[b], n, 0, stride, seed + b, 0, 1, 0, lo, hi)
+        torch.cuda.synchronize()
+
+    def launch(v, b):
+        u = slab[b * bb:(b + 1) * bb]
+        if v < 0:
+            X.echo_dev(u, descs[b], n, verd, recs, stats, ws, stream)
+        else:
+            rc = tune.xsk_gpu__echo_variant(v, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n, verd.data_ptr(),
+                                            recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
+            assert rc == 0, rc
+
+    # warm-up: every variant once on a batch that is then regenerated
+    regen()
+    for i, v in enumerate(V):
+        launch(v, i % pool)
+    times = {v: [] for v in V}
+    for r in range(args.rounds):
+        regen()
+        evs = []
+        for b in range(pool):
+            v = V[(b + r) % len(V)]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            launch(v, b)
+            e1.record(stream)
+            evs.append((v, e0, e1))
+        torch.cuda.synchronize()
+        for v, e0, e1 in evs:
+            times[v].append(e0.elapsed_time(e1) * 1000.0)
+        print(json.dumps({"round": r, **{str(v): round(float(np.median(times[v][-pool // len(V):])), 2) for v in V}}),
+              flush=True)
+    out = {"config": args.config, "pool": pool, "rounds": args.rounds, "desc": desc}
+    for v in V:
+        t = np.sort(np.array(times[v]))
+        k = len(t) // 8
+        out[str(v)] = {"median_us": round(float(np.median(t)), 2), "mean_us": round(float(t.mean()), 2),
+                       "trim_mean_us": round(float(t[k:len(t) - k].mean()), 2), "min_us": round(float(t[0]), 2),
+                       "n": int(len(t))}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

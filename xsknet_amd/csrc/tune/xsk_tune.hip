@@ -462,6 +462,19 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             // 137 / 138: shipped + the penultimate round's windows deferred to the end (DEFW 1: heavy waves; 2: all)
             case 137: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 138: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 2><<<gg, bb, 0, s>>>(args, per); break;
+            // 139 / 140: diagnostics (wrong results): 137 dropping the deferred windows / re-reading them only
+            case 139: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 3><<<gg, bb, 0, s>>>(args, per); break;
+            case 140: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 4><<<gg, bb, 0, s>>>(args, per); break;
+            // 141-143: the shipped kernel's read phase alone (NOWR, wrong results) with the next tile's descriptors
+            // prefetched (141), without the round waits (142: SYNC 0), both (143); 144: 131 + PF
+            case 141: echo_kernel6<4, 2, 2, 2, true, false, false, false, true, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 142: echo_kernel6<4, 2, 0, 2, false, false, false, false, true, true, true, true, false, false, 0, 1, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 143: echo_kernel6<4, 2, 0, 2, true, false, false, false, true, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 144: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true, true, true, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 145: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, 1, true><<<gg, bb, 0, s>>>(args, per); break;
+            // 146: 131 + the round-level descriptor prefetch (RPF); 147: its read phase alone (NOWR)
+            case 146: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, true><<<gg, bb, 0, s>>>(args, per); break;
+            case 147: echo_kernel6<4, 2, 2, 2, false, false, false, false, true, true, true, true, false, false, 0, 1, true, false, false, 0, true><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

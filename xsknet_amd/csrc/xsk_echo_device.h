@@ -1146,13 +1146,19 @@ template <bool SYNC2>
 __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0, uint32_t t1, uint8_t* rows0,
                                                   uint8_t* rows1, uint32_t* sums0, uint32_t* sums1, uint32_t lane,
                                                   Counters& cnt, u32x4* rec, uint32_t* verd, uint32_t* alo,
-                                                  uint32_t* ahi, uint64_t* wbm, uint32_t& round_long) {
+                                                  uint32_t* ahi, uint64_t* wbm, uint32_t& round_long,
+                                                  const u32x4* pre = nullptr) {
     if (a.front) return false;
     const uint32_t fi0 = t0 * kTile + lane, fi1 = t1 * kTile + lane;
     const bool in0 = fi0 < a.n, in1 = fi1 < a.n;
     u32x4 d0 = u32x4{0u, 0u, 0u, 0u}, d1 = u32x4{0u, 0u, 0u, 0u};
-    if (in0) d0 = *(const u32x4*)(a.descs + fi0);
-    if (in1) d1 = *(const u32x4*)(a.descs + fi1);
+    if (pre) {  // RPF: the round's descriptors were prefetched during the previous round
+        if (in0) d0 = pre[0];
+        if (in1) d1 = pre[1];
+    } else {
+        if (in0) d0 = *(const u32x4*)(a.descs + fi0);
+        if (in1) d1 = *(const u32x4*)(a.descs + fi1);
+    }
     const FrameIn F0 = frame_in(a, d0, in0), F1 = frame_in(a, d1, in1);
     if ((__ballot(F0.lim > (uint32_t)kWin) | __ballot(F1.lim > (uint32_t)kWin)) != 0ull) return false;
     const uint32_t kk = lane & 3u, ro = 16u * kk;
@@ -1226,7 +1232,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, bool RPF = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1281,6 +1287,31 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     uint64_t dwbm[TPW];
     uint32_t dalo[TPW], dahi[TPW];
     bool have_def = false;  // wave-uniform
+    // RPF: the descriptors of a wave's next-round tiles are loaded at the start of the current round (one
+    // 16-B load per lane and tile), so a round's first memory round trip is its frames, not its descriptors
+    static_assert(!RPF || (!PF && !DYN && !SUBT && !DLDS && VT == 0 && SYNC < 3), "round prefetch: static shares");
+    u32x4 rnext[TPW], rcur[TPW];
+    auto phys_tile = [&](uint32_t t) -> uint32_t {  // the read / write phases' tile mapping; ~0u: none
+        if (!SUBT && !DYN && a.front) {
+            t = front_tile(a, t);
+            if (t >= (a.n + kTile - 1) / kTile) return ~0u;
+        }
+        if (!SUBT && !DYN && a.rot) t = rot_tile(a, t, t_begin, t_end);
+        return t;
+    };
+    auto prefetch_round = [&](uint32_t rb) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            rnext[i] = u32x4{0u, 0u, 0u, 0u};
+            const uint32_t tl = rb + (uint32_t)i * NW + wave;
+            if (tl < t_end) {
+                const uint32_t t = phys_tile(tl);
+                const uint32_t fi = t * (uint32_t)kTile + lane;
+                if (t != ~0u && fi < a.n) rnext[i] = *(const u32x4*)(a.descs + fi);
+            }
+        }
+    };
+    if (RPF) prefetch_round(t_begin);
     uint32_t r0 = t_begin;
     for (;;) {  // rounds, workgroup-uniform
         // slot i of this round: wave w streams tile ub[i] + w when it is below ue[i]
@@ -1303,6 +1334,14 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 ue[i] = t_end;
             }
             r0 += kRound;
+        }
+        // RPF: the next round's descriptors are loaded once this round's own loads are out -- before the last
+        // tile's stream, or after the paired short tiles' reads -- so waiting for them never waits for the prefetch
+        bool rpf_due = false;
+        if (RPF) {
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) rcur[i] = rnext[i];
+            rpf_due = r0 < r_end;
         }
         // CARRY: the tile carried out of the previous round is written in this round's write phase
         const bool carried_prev = CARRY && carried;
@@ -1328,7 +1367,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             paired = read_round_short2<SYNC == 2>(a, (!SUBT && !DYN && a.rot) ? rot_tile(a, ub[0] + wave, t_begin, t_end) : ub[0] + wave,
                                                   (!SUBT && !DYN && a.rot) ? rot_tile(a, ub[1] + wave, t_begin, t_end) : ub[1] + wave, s_hdr[wave][0], s_hdr[wave][TPW > 1 ? 1 : 0],
                                                   sm.sum[wave][0], sm.sum[wave][1], lane, cnt, rec, verd, alo, ahi,
-                                                  wbm, round_long);
+                                                  wbm, round_long, RPF ? rcur : nullptr);
+        if (RPF && paired && rpf_due) {
+            prefetch_round(r0);
+            rpf_due = false;
+        }
         constexpr int kReadUnroll = VT > 0 ? 1 : TPW;
 #pragma unroll kReadUnroll
         for (int i = 0; i < TPW; ++i) {
@@ -1359,7 +1402,9 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 const bool in_n = (!SUBT || lane < a.tile_live) && fi < a.n;  // a live frame of the batch
                 // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
                 u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
-                if (PF) {
+                if (RPF) {
+                    if (in_n) dsc = rcur[i];
+                } else if (PF) {
                     dsc = dnext;
                     const uint32_t tn = i + 1 < TPW ? t + (uint32_t)NW : r0 + wave;  // next tile (r0: next round)
                     const uint32_t fn = tn * kTile + lane;
@@ -1409,6 +1454,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 ahi_o = dsc.y;
                 if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= kHeavyLen));
 
+                if (RPF && i == TPW - 1 && rpf_due) {  // the last tile's descriptors are in: prefetch the next round
+                    prefetch_round(r0);
+                    rpf_due = false;
+                }
                 if (TRACE && threadIdx.x == 0 && i == 0) a.trace[0] = wall_clock64();  // descriptors parsed
                 // ---- 2. stream every row byte once; windows -> LDS rows, row sums -> LDS -----------------
                 if (__ballot(nit != 0u) != 0ull) {
@@ -1605,6 +1654,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             }
         }
 
+        if (RPF && rpf_due) prefetch_round(r0);  // this wave had no last tile this round
         if (TRACE && threadIdx.x == 0) a.trace[2] = wall_clock64();  // header phase done
         // ================= write phase: every wave of the workgroup has finished reading =================
         if (SYNC == 1) __syncthreads();
@@ -1748,7 +1798,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             __syncthreads();
         }
     }
-    if (DEFW && have_def) {  // the deferred windows: re-read (unchanged since), re-patched, written
+    // (DEFW 3 / 4 are diagnostics with wrong results: 3 drops the deferred windows, 4 re-reads them only)
+    if (DEFW && DEFW != 3 && have_def) {  // the deferred windows: re-read (unchanged since), re-patched, written
         u32x4 x[TPW][4];
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
@@ -1769,6 +1820,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 const uint32_t f = (uint32_t)r * 16u + (lane >> 2), kk = lane & 3u;
                 *(u32x4*)(s_hdr[wave][i] + f * kWin + 16u * kk) = x[i][r];
             }
+        if (DEFW == 4) {
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) dwbm[i] = 0ull;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1807,7 +1862,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false,
-          int DEFW = 0>
+          int DEFW = 0, bool RPF = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1817,7 +1872,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR, RD2, CARRY, DEFW>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2, CARRY, DEFW, RPF>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
