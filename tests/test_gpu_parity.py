@@ -268,16 +268,12 @@ def test_small_batches_share_stats_across_streams():
     assert (d_umem.cpu().numpy() == ref).all()
 
 
-@pytest.mark.parametrize("frames", ["mixed", "c1_64"])
 @pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT])
-def test_host_umem_modes(mode, frames):
-    """C1 shape: 4096 frames in a 16 MiB UMEM of 4 KiB chunks (xsk_utils.h:6-7), RX batches of 64
-    (RX_BATCH_SIZE, xsk_utils.h:8) and one big batch.  "c1_64" is BASELINE config 1 exactly: 4096 valid
-    64-B echo requests; "mixed" adds every negative / edge case at 20-1500 B."""
+def test_host_umem_modes(mode):
+    """C1 shape: 4096 frames in a 16 MiB UMEM of 4 KiB chunks, RX batches of 64 (and one big batch)."""
     n = 4096
     umem = np.zeros(4096 * 4096, np.uint8)
-    smode, lo, hi = (1, 20, 1500) if frames == "mixed" else (0, 64, 64)
-    descs = oracle.synth_batch(umem, n, 256, 4096, seed=0x5EED0001, mode=smode, len_lo=lo, len_hi=hi)
+    descs = oracle.synth_batch(umem, n, 256, 4096, seed=0x5EED0001, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
     for batch in (64, 4096):
@@ -296,8 +292,6 @@ def test_host_umem_modes(mode, frames):
         for k in tot:
             assert tot[k] == int(s_ref[k])
         assert (work == ref).all(), np.nonzero(work != ref)[0][:8]
-    if frames == "c1_64":
-        assert (v_ref == 0).all()
 
 
 def test_echo_replay_tool():
