@@ -1232,7 +1232,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, bool RPF = false>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, bool RPF = false, int DIAG = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1605,8 +1605,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
                 const uint32_t ip_raw = nit ? sums_ip[lane] : 0u;
-                bool wb;
-                if (WIRE)
+                bool wb = false;
+                if (DIAG & 1) {  // diagnostic (wrong results): no header phase at all
+                    rec_o = u32x4{ic_raw, ip_raw, 0u, 0u};
+                } else if (WIRE)
                     wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
                                            &verd_o);
                 else
@@ -1862,7 +1864,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false,
-          int DEFW = 0, bool RPF = false>
+          int DEFW = 0, bool RPF = false, int DIAG = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1872,7 +1874,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR, RD2, CARRY, DEFW, RPF>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2, CARRY, DEFW, RPF, DIAG>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
