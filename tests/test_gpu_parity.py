@@ -495,6 +495,43 @@ def test_uniform_tile_streams(variant, flen):
             d_umem.copy_(to_dev(umem))
 
 
+@pytest.mark.parametrize("variant", [131])
+@pytest.mark.parametrize("case", ["packed64", "mixed_short", "one_long"])
+@pytest.mark.parametrize("grid", [1, 2, 3])
+def test_short_tile_rounds(variant, case, grid):
+    """Shares of several rounds of short tiles (every frame within its 64-B window) on 1-3 workgroups, so that
+    the paired short-tile path (PAIR) runs for real in every round of a share: 9000 frames = 141 tiles, a
+    partial last tile; "one_long" puts one 200-B frame in a second-round tile (that round falls back to the
+    row streams), "mixed_short" adds every negative case at odd offsets."""
+    L = X.tune_lib()
+    dev = _dev()
+    n = 9000
+    if case == "packed64":
+        stride, off, mode, lo, hi = 64, 0, 0, 64, 64
+    else:
+        stride, off, mode, lo, hi = 256, 3, 1 if case == "mixed_short" else 0, 20, 48
+    umem = np.zeros(n * stride + 1024, np.uint8)
+    descs = oracle.synth_batch(umem, n, off, stride, seed=0x5EED2222 + stride, mode=mode, len_lo=lo, len_hi=hi)
+    if case == "one_long":
+        descs["len"][64 * 40 + 9] = 200  # tile 40: the second round of workgroup 0 at grid 1
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    d_umem, d_descs = to_dev(umem), to_dev(descs)
+    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    rc = L.xsk_gpu__echo_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                 d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (d_verd.cpu().numpy() == v_ref).all()
+    assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+    assert (d_umem.cpu().numpy() == ref).all()
+    part = ws[:grid * 32].cpu().numpy().view(np.uint64).reshape(grid, 4).sum(axis=0)
+    assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
+
+
 def test_dynamic_schedule_full_size_and_reuse():
     """The dynamic schedules (tuning variants 93 / 95: per-XCD rounds; 99: a tail pool) over 1 M mixed frames, three launches on one
     workspace: every frame exact each time (the counters reset themselves between launches)."""
