@@ -428,7 +428,7 @@ def test_timing_hook():
     assert cnt == 3 and ms > 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96, 99, 101, 103, 104, 107, 108, 110, 111, 112, 113, 116, 117, 118, 119, 121, 122, 123, 125, 126, 130, 131, 132, 133, 134, 135, 136, 137, 138, 144, 146])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74, 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96, 99, 101, 103, 104, 107, 108, 110, 111, 112, 113, 116, 117, 118, 119, 121, 122, 123, 125, 126, 130, 131, 132, 133, 134, 135, 136, 137, 138, 144, 146, 151])
 @pytest.mark.parametrize("grid", [0, 1, 7])
 @pytest.mark.parametrize("len_hi", [2048, 112, 48])
 def test_kernel_variants_parity(variant, grid, len_hi):
@@ -462,7 +462,7 @@ def test_kernel_variants_parity(variant, grid, len_hi):
         assert int(ws[768 << 10:(768 << 10) + 36].sum().item()) == 0
 
 
-@pytest.mark.parametrize("variant", [92, 119, 121, 123, 125, 126, 133, 135, 136, 137, 138, 146])
+@pytest.mark.parametrize("variant", [92, 119, 121, 123, 125, 126, 133, 135, 136, 137, 138, 146, 151])
 @pytest.mark.parametrize("flen", [20, 33, 42, 63, 64, 100, 256, 300, 769, 1024, 1500, 4000, 9000])
 def test_uniform_tile_streams(variant, flen):
     """Tiles whose frames all share one length and one 16-B offset (the uniform long-tile stream, ULONG: byte
@@ -495,8 +495,8 @@ def test_uniform_tile_streams(variant, flen):
             d_umem.copy_(to_dev(umem))
 
 
-@pytest.mark.parametrize("variant", [131])
-@pytest.mark.parametrize("case", ["packed64", "mixed_short", "one_long"])
+@pytest.mark.parametrize("variant", [131, 146, 151])
+@pytest.mark.parametrize("case", ["packed64", "mixed_short", "one_long", "ragged"])
 @pytest.mark.parametrize("grid", [1, 2, 3])
 def test_short_tile_rounds(variant, case, grid):
     """Shares of several rounds of short tiles (every frame within its 64-B window) on 1-3 workgroups, so that
@@ -508,6 +508,8 @@ def test_short_tile_rounds(variant, case, grid):
     n = 9000
     if case == "packed64":
         stride, off, mode, lo, hi = 64, 0, 0, 64, 64
+    elif case == "ragged":  # ranked streams in every round (the adaptive descriptor prefetch, 151)
+        stride, off, mode, lo, hi = 2048, 0, 1, 20, 1500
     else:
         stride, off, mode, lo, hi = 256, 3, 1 if case == "mixed_short" else 0, 20, 48
     umem = np.zeros(n * stride + 1024, np.uint8)

@@ -1232,7 +1232,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, bool RPF = false, int DIAG = 0>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, int RPF = 0, int DIAG = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1311,7 +1311,13 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             }
         }
     };
-    if (RPF) prefetch_round(t_begin);
+    // RPF 2 (adaptive): only a wave whose round streamed a ragged tile (ranked stream) prefetches the next
+    // round's descriptors -- ragged tiles are short enough for a descriptor round trip to show
+    bool have_pf = false;  // wave-uniform: rnext holds the next round's descriptors
+    if (RPF == 1) {
+        prefetch_round(t_begin);
+        have_pf = true;
+    }
     uint32_t r0 = t_begin;
     for (;;) {  // rounds, workgroup-uniform
         // slot i of this round: wave w streams tile ub[i] + w when it is below ue[i]
@@ -1337,10 +1343,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         }
         // RPF: the next round's descriptors are loaded once this round's own loads are out -- before the last
         // tile's stream, or after the paired short tiles' reads -- so waiting for them never waits for the prefetch
-        bool rpf_due = false;
+        bool rpf_due = false, cur_pf = false, ragged = false;
         if (RPF) {
 #pragma unroll
             for (int i = 0; i < TPW; ++i) rcur[i] = rnext[i];
+            cur_pf = have_pf;
+            have_pf = false;
             rpf_due = r0 < r_end;
         }
         // CARRY: the tile carried out of the previous round is written in this round's write phase
@@ -1367,9 +1375,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             paired = read_round_short2<SYNC == 2>(a, (!SUBT && !DYN && a.rot) ? rot_tile(a, ub[0] + wave, t_begin, t_end) : ub[0] + wave,
                                                   (!SUBT && !DYN && a.rot) ? rot_tile(a, ub[1] + wave, t_begin, t_end) : ub[1] + wave, s_hdr[wave][0], s_hdr[wave][TPW > 1 ? 1 : 0],
                                                   sm.sum[wave][0], sm.sum[wave][1], lane, cnt, rec, verd, alo, ahi,
-                                                  wbm, round_long, RPF ? rcur : nullptr);
-        if (RPF && paired && rpf_due) {
+                                                  wbm, round_long, (RPF && cur_pf) ? rcur : nullptr);
+        if (RPF == 1 && paired && rpf_due) {
             prefetch_round(r0);
+            have_pf = true;
             rpf_due = false;
         }
         constexpr int kReadUnroll = VT > 0 ? 1 : TPW;
@@ -1402,7 +1411,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 const bool in_n = (!SUBT || lane < a.tile_live) && fi < a.n;  // a live frame of the batch
                 // ---- 1. descriptors (xsk_receive.c:222-223): lane i <- frame t*64+i ----------------------
                 u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
-                if (RPF) {
+                if (RPF && cur_pf) {
                     if (in_n) dsc = rcur[i];
                 } else if (PF) {
                     dsc = dnext;
@@ -1454,8 +1463,9 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 ahi_o = dsc.y;
                 if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= kHeavyLen));
 
-                if (RPF && i == TPW - 1 && rpf_due) {  // the last tile's descriptors are in: prefetch the next round
-                    prefetch_round(r0);
+                if (RPF && i == TPW - 1 && rpf_due && (RPF == 1 || ragged)) {  // the last tile's descriptors are in:
+                    prefetch_round(r0);                                          // prefetch the next round's
+                    have_pf = true;
                     rpf_due = false;
                 }
                 if (TRACE && threadIdx.x == 0 && i == 0) a.trace[0] = wall_clock64();  // descriptors parsed
@@ -1558,6 +1568,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                                (STREAM == 2 && (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                                 uniform(max_nit_lane(nit)) < (uint32_t)U))) {
                         // (the dot2 sums measured ~1 % slower in the ranked streams: the 64-bit adds stay there)
+                        ragged = true;
                         if (fast) stream_tile_sorted<U, true, WIRE, RD2 && !WIRE, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                         else stream_tile_sorted<U, false, WIRE, RD2 && !WIRE, SKM>(a, ld.r, meta, s_sort[wave], rows, sums_ic, nit, lane);
                     } else if (ULONG && (WIRE || STREAM >= 1) && fast && __ballot(!parse) == 0ull &&
@@ -1656,7 +1667,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             }
         }
 
-        if (RPF && rpf_due) prefetch_round(r0);  // this wave had no last tile this round
+        if (RPF == 1 && rpf_due) {  // this wave had no last tile this round
+            prefetch_round(r0);
+            have_pf = true;
+        }
         if (TRACE && threadIdx.x == 0) a.trace[2] = wall_clock64();  // header phase done
         // ================= write phase: every wave of the workgroup has finished reading =================
         if (SYNC == 1) __syncthreads();
@@ -1864,7 +1878,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false,
-          int DEFW = 0, bool RPF = false, int DIAG = 0>
+          int DEFW = 0, int RPF = 0, int DIAG = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
