@@ -480,6 +480,9 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 149: echo_kernel6<4, 2, 2, 2, true, false, false, false, true, true, true, true, false, false, 0, 1, false, false, false, 0, false, 1><<<gg, bb, 0, s>>>(args, per); break;
             // 151: 131 + the adaptive round prefetch (RPF 2: waves that streamed a ragged tile this round)
             case 151: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            // 152 / 153: 131 with write-through (sc1) window stores / window and record stores (WT 1 / 2)
+            case 152: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 153: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

@@ -80,6 +80,7 @@ __device__ __forceinline__ uint32_t rot_tile(const EchoArgs& a, uint32_t t, uint
 // Buffer-resource word 3 for gfx950 raw buffers (cdna_hip_programming.md §5.5 T8).
 constexpr int kRsrcFlags = 0x00020000;
 constexpr int kAuxNT = 2;  // nontemporal: payload bytes are read exactly once
+constexpr int kAuxSC1 = 16;  // sc1 (gfx940+ cache policy): write-through past the XCD's L2
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);  // keep it unsigned: no sign-extension
@@ -462,6 +463,7 @@ constexpr bool kShip6D2 = true;             // v_dot2_u32_u16 sums of halves (sh
 constexpr bool kShip6Skm = true;            // ranked streams mask only slots where a frame ends
 constexpr int kShip6Ulong = 1;              // uniform long tiles: byte masks once per tile (stream_tile_uniform)
 constexpr bool kShip6Pair = true;           // both tiles of a round read at once when all frames fit their windows
+constexpr int kShip6Wt = 2;                 // write-phase windows and records stored write-through (sc1)
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -1232,7 +1234,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, int RPF = 0, int DIAG = 0>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, int RPF = 0, int DIAG = 0, int WT = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1318,6 +1320,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         prefetch_round(t_begin);
         have_pf = true;
     }
+    // WT: write-phase stores write-through (sc1: the line leaves the XCD's L2 at once instead of staying
+    // dirty until the next round's reads evict it, so the write phase really is one); 1 = windows, 2 = windows
+    // and records.  They are raw buffer stores (the only 16-B store that takes a cache policy): a tile's
+    // windows through a buffer based at the 4 GiB-aligned UMEM region its frames share (32-bit offsets; a tile
+    // whose windows straddle regions takes plain stores), its records through a buffer at the tile's first record.
     uint32_t r0 = t_begin;
     for (;;) {  // rounds, workgroup-uniform
         // slot i of this round: wave w streams tile ub[i] + w when it is below ue[i]
@@ -1749,6 +1756,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 dahi[i] = ahi[qi];
             }
             if (wbm[qi] && !(DEFW && defer)) {  // patched windows: 16 frames x 64 B per wave-store, whole 64-B sectors
+                // WT: the 4 GiB region of the tile's first written window; every written window inside it?
+                const uint32_t hi_u = WT ? rdlane(ahi[qi], (uint32_t)__builtin_ctzll(wbm[qi])) : 0u;
+                const bool wt_tile = WT && __ballot(((wbm[qi] >> lane) & 1ull) &&
+                                                    (ahi[qi] != hi_u || alo[qi] > 0xFFFFFFC0u)) == 0ull;
+                const __amdgpu_buffer_rsrc_t wrs =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + ((uint64_t)hi_u << 32)), (short)0, -1, kRsrcFlags);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
@@ -1758,7 +1771,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     if ((wbm[qi] >> f) & 1ull) {
                         const uint64_t fa = (uint64_t)flo | ((uint64_t)fhi << 32);
                         const u32x4 w = *(const u32x4*)(rows + f * kRowW + 16u * kk);
-                        if (NTS) __builtin_nontemporal_store(w, (u32x4*)(a.umem + fa + 16u * kk));
+                        if (WT && wt_tile) __builtin_amdgcn_raw_buffer_store_b128(w, wrs, (int)(flo + 16u * kk), 0, kAuxSC1);
+                        else if (NTS) __builtin_nontemporal_store(w, (u32x4*)(a.umem + fa + 16u * kk));
                         else *(u32x4*)(a.umem + fa + 16u * kk) = w;
                     }
                 }
@@ -1766,7 +1780,13 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
             if ((!SUBT || lane < a.tile_live) && fi < a.n) {
                 if (a.recs) {
-                    if (NTS) __builtin_nontemporal_store(rec[qi], (u32x4*)a.recs + fi);
+                    if (WT >= 2)
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            rec[qi],
+                            __builtin_amdgcn_make_buffer_rsrc((void*)((u32x4*)a.recs + (uint64_t)uniform(t) * (SUBT ? a.tile_live : (uint32_t)kTile)),
+                                                              (short)0, -1, kRsrcFlags),
+                            (int)(lane * 16u), 0, kAuxSC1);
+                    else if (NTS) __builtin_nontemporal_store(rec[qi], (u32x4*)a.recs + fi);
                     else ((u32x4*)a.recs)[fi] = rec[qi];
                 }
                 if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[qi];
@@ -1878,7 +1898,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false,
-          int DEFW = 0, int RPF = 0, int DIAG = 0>
+          int DEFW = 0, int RPF = 0, int DIAG = 0, int WT = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1888,7 +1908,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR, RD2, CARRY, DEFW, RPF, DIAG>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2, CARRY, DEFW, RPF, DIAG, WT>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
