@@ -31,9 +31,9 @@ import torch  # noqa: E402
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # the transform kernel xsk_gpu_echo_dev launches for a large batch (the name rocprofv3 reports)
-KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2>"
+KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512>"
 # xsk_gpu_echo_dev_opts, nonzero --opts
-WIRE_KERNEL = "echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 0>"
+WIRE_KERNEL = "echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2, 1024>"
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
@@ -229,7 +229,7 @@ def _kname(k):
         return k
     base, args = k[:-1].split("<", 1)
     a = [x.strip() for x in args.split(",")]
-    while a and a[-1] in ("false", "0"):
+    while a and a[-1] in ("false", "0", "1024"):  # 1024: HEAVY's default (xsk_echo_device.h kHeavyLen)
         a.pop()
     return base + "<" + ", ".join(a) + ">"
 

@@ -190,3 +190,42 @@ def test_wire_multi_round_mixed():
         descs[i] = (a, L, 0)
     v = check(umem, descs, X.OPT_ALL)
     assert (v == X.DROP_BAD_IP).any() and (v == 0).any()
+
+
+@pytest.mark.parametrize("variant", [160, 161])
+@pytest.mark.parametrize("grid", [1, 3])
+def test_wire_tuning_variants(variant, grid):
+    """The wire-mode round kernel from the tuning library (160: as shipped, 161: write-through write phases)
+    on mixed wire traffic, shares of many rounds (1-3 workgroups), every option on, against the oracle."""
+    from tests.wire_frames import random_frame
+    dev = _dev()
+    L = X.tune_lib()
+    rng = np.random.default_rng(4242)
+    pool = []
+    while len(pool) < 512:
+        f, ln = random_frame(rng)
+        pool.append((np.frombuffer(f, np.uint8), ln))
+    n, stride = 20_000, 2048
+    umem = rng.integers(0, 256, n * stride + 256, dtype=np.uint8)
+    descs = np.zeros(n, oracle.DESC_DTYPE)
+    for i in range(n):
+        fr, ln = pool[(i * 7919) % len(pool)]
+        a = i * stride + (i % 16)
+        umem[a:a + fr.size] = fr
+        descs[i] = (a, ln, 0)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
+    d_umem, d_descs = to_dev(umem), to_dev(np.ascontiguousarray(descs, X.DESC_DTYPE))
+    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    rc = L.xsk_gpu__echo_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                 d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (d_verd.cpu().numpy() == v_ref).all()
+    assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+    assert (d_umem.cpu().numpy() == ref).all()
+    part = ws[:grid * 32].cpu().numpy().view(np.uint64).reshape(grid, 4).sum(axis=0)
+    assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]

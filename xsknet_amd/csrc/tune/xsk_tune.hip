@@ -363,6 +363,7 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         }
         if (variant == 134 || variant == 136) args.rot = 37;  // 131 with rotated shares
         if (variant == 135 || variant == 136) args.srot = 5;  // 131 with rotated uniform-stream steps
+        if (variant == 160 || variant == 161) args.opts = XSK_GPU_OPT_ALL;  // the wire-mode kernel, every option
         if (variant == 90 || variant == 91 || variant == 128 || variant == 129) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
             if (!d_workspace) return -EINVAL;
             HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
@@ -483,6 +484,17 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             // 152 / 153: 131 with write-through (sc1) window stores / window and record stores (WT 1 / 2)
             case 152: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 153: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            // 154-157: the shipped kernel (153, write-through) with SYNC 0 / SYNC 1 / PF instead of PAIR / one
+            // tile per wave per round; 160 / 161: the wire-mode kernel (opts = all) plain / write-through
+            case 154: echo_kernel6<4, 2, 0, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 155: echo_kernel6<4, 2, 1, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 156: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true, true, true, false, false, 0, 1, false, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            case 157: echo_kernel6<4, 1, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, false, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            // 158 / 159: the shipped kernel with the SYNC 2 heavy-frame length at 512 / 256 B (c4's waves then wait)
+            case 158: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            case 159: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 256><<<gg, bb, 0, s>>>(args, per); break;
+            case 160: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
+            case 161: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

@@ -191,14 +191,16 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     const int slot = timer_begin(device, s);
     if (opts == 0 && !small)
         echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2,
-                     kShip6Skm, false, false, 0, kShip6Ulong, kShip6Pair, false, false, 0, 0, 0, kShip6Wt>
+                     kShip6Skm, false, false, 0, kShip6Ulong, kShip6Pair, false, false, 0, 0, 0, kShip6Wt,
+                     kShip6Heavy>
             <<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (opts == 0)  // one round of sub-tiles, writes as soon as a wave has read
         echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2, kShip6Skm,
                      true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (!small)  // wire mode: 128-B windows, one tile per wave per round
         echo_kernel6<kShip6U, 1, kShip6Sync, kShip6Stream, false, false, true, false, false, false, false, false, false,
-                     false, 0, kShip6Ulong><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+                     false, 0, kShip6Ulong, false, false, false, 0, 0, 0, kShip6Wt><<<dim3(grid), dim3(kThreads6), 0, s>>>(
+            args, tiles_per_wg);
     else
         echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, true, false, false, false, false, false, true>
             <<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);

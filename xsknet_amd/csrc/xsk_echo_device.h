@@ -464,6 +464,7 @@ constexpr bool kShip6Skm = true;            // ranked streams mask only slots wh
 constexpr int kShip6Ulong = 1;              // uniform long tiles: byte masks once per tile (stream_tile_uniform)
 constexpr bool kShip6Pair = true;           // both tiles of a round read at once when all frames fit their windows
 constexpr int kShip6Wt = 2;                 // write-phase windows and records stored write-through (sc1)
+constexpr int kShip6Heavy = 512;            // SYNC 2: a wave most of whose frames have >= 512 B waits for the round
 
 // 16-B per-frame stream metadata (the header phase keeps addr/len in the owning lane's VGPRs).
 struct FrameMeta6 {
@@ -1013,7 +1014,9 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
 }
 
 // SYNC: how a wave enters its write phase.  0: at once; 1: workgroup barrier (all waves read, then
-// all write); 2: a wave at least half of whose frames this round had >= kHeavyLen bytes waits until every wave of
+// all write); 2: a wave at least half of whose frames this round had >= HEAVY bytes (template parameter; default
+// kHeavyLen, the shipped reference-mode kernel 512 -- with write-through write phases c4's waves gain from
+// waiting too: DESIGN.md §4) waits until every wave of
 // the workgroup has finished reading the round (LDS arrival counter), lighter waves go ahead -- the
 // phase separation pays where reads dominate, and costs latency hiding where frames are short.
 // 3 / 4 (tuning only): a chip-wide barrier before (3) or around (4) every write phase, on a counter the
@@ -1234,7 +1237,8 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, bool TRACE = false, bool DLDS = false, int NW = kWaves6, int VT = 0, int ULONG = 0,
-          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, int RPF = 0, int DIAG = 0, int WT = 0>
+          bool PAIR = false, bool RD2 = false, bool CARRY = false, int DEFW = 0, int RPF = 0, int DIAG = 0, int WT = 0,
+          int HEAVY = (int)kHeavyLen>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, uint32_t tiles_per_wg,
                                            Echo6Smem<TPW, WIRE, STREAM, NW, TPW - VT>& sm) {
     static_assert(!DYN || (!PF && SYNC < 3 && !SUBT && NW == kWaves6), "the dynamic schedule takes no prefetch / grid barrier / sub-tiles");
@@ -1468,7 +1472,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 }
                 alo_o = dsc.x;
                 ahi_o = dsc.y;
-                if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= kHeavyLen));
+                if (SYNC == 2) round_long += (uint32_t)__popcll(__ballot(in_n && len >= (uint32_t)HEAVY));
 
                 if (RPF && i == TPW - 1 && rpf_due && (RPF == 1 || ragged)) {  // the last tile's descriptors are in:
                     prefetch_round(r0);                                          // prefetch the next round's
@@ -1898,7 +1902,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 template <int U, int TPW, int SYNC = 1, int STREAM = 0, bool PF = false, bool WGT = false, bool WIRE = false,
           bool NTS = false, bool NOWR = false, bool MID = false, bool D2 = false, bool SKM = false, bool SUBT = false,
           bool DYN = false, int TAIL = 0, int ULONG = 0, bool PAIR = false, bool RD2 = false, bool CARRY = false,
-          int DEFW = 0, int RPF = 0, int DIAG = 0, int WT = 0>
+          int DEFW = 0, int RPF = 0, int DIAG = 0, int WT = 0, int HEAVY = (int)kHeavyLen>
 __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_t tiles_per_wg) {
     __shared__ Echo6Smem<TPW, WIRE, STREAM> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
@@ -1908,7 +1912,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_kernel6(EchoArgs a, uint32_
         const uint32_t t_begin = a.front ? 0u : blockIdx.x * tiles_per_wg;
         const uint32_t t_end = a.front ? tiles_per_wg : min(ntiles, t_begin + tiles_per_wg);
         echo6_body<U, TPW, SYNC, STREAM, PF, WGT, WIRE, NTS, NOWR, MID, D2, SKM, SUBT, DYN, false, false, kWaves6, 0,
-                   ULONG, PAIR, RD2, CARRY, DEFW, RPF, DIAG, WT>(a, t_begin, t_end, tiles_per_wg, sm);
+                   ULONG, PAIR, RD2, CARRY, DEFW, RPF, DIAG, WT, HEAVY>(a, t_begin, t_end, tiles_per_wg, sm);
         return;
     }
     static_assert(TAIL == 0 || (!SUBT && !DYN && !PF && SYNC < 3), "the tail pool runs on plain static shares");
