@@ -192,7 +192,7 @@ def test_wire_multi_round_mixed():
     assert (v == X.DROP_BAD_IP).any() and (v == 0).any()
 
 
-@pytest.mark.parametrize("variant", [160, 161])
+@pytest.mark.parametrize("variant", [160, 161, 162])
 @pytest.mark.parametrize("grid", [1, 3])
 def test_wire_tuning_variants(variant, grid):
     """The wire-mode round kernel from the tuning library (160: as shipped, 161: write-through write phases)

@@ -363,7 +363,7 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         }
         if (variant == 134 || variant == 136) args.rot = 37;  // 131 with rotated shares
         if (variant == 135 || variant == 136) args.srot = 5;  // 131 with rotated uniform-stream steps
-        if (variant == 160 || variant == 161) args.opts = XSK_GPU_OPT_ALL;  // the wire-mode kernel, every option
+        if (variant >= 160 && variant <= 162) args.opts = XSK_GPU_OPT_ALL;  // the wire-mode kernel, every option
         if (variant == 90 || variant == 91 || variant == 128 || variant == 129) {  // chip-wide barrier counter (workspace + 512 KiB), zeroed
             if (!d_workspace) return -EINVAL;
             HIP_TRY(hipMemsetAsync((uint8_t*)d_workspace + 65536 * 8, 0, 64, s));
@@ -495,6 +495,8 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 159: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 256><<<gg, bb, 0, s>>>(args, per); break;
             case 160: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
             case 161: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
+            // 162: 161 (wire mode, write-through) with the 512-B heavy threshold
+            case 162: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
