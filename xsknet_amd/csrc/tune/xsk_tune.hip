@@ -497,6 +497,12 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 161: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2><<<gg, bb, 0, s>>>(args, per); break;
             // 162: 161 (wire mode, write-through) with the 512-B heavy threshold
             case 162: echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            // 163: the shipped kernel (write-through, 512-B heavy threshold) as a tuning variant; 164 / 165 with
+            // the round-level descriptor prefetch (RPF 1 / 2); 166 with PF instead of PAIR
+            case 163: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            case 164: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 1, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            case 165: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 2, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            case 166: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true, true, true, false, false, 0, 1, false, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
