@@ -729,3 +729,50 @@ def test_tile_spanning_more_than_2gib(mode, lo, hi, opts):
     assert (recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
     assert (d_umem[:n * 2048 + 64].cpu().numpy() == img[:n * 2048 + 64]).all()
     assert (d_umem[far:far + n * 2048 + 64].cpu().numpy() == img[n * 2048 + 64:]).all()
+
+
+def test_write_through_across_4gib_regions():
+    """The write phase's write-through stores address a tile's windows from the 4 GiB-aligned UMEM region they
+    share: tiles whose windows lie in two regions, tiles wholly above 4 GiB, and a window that straddles the
+    4 GiB line itself (plain stores for those tiles) -- every byte against the oracle (large-batch kernel)."""
+    dev = _dev()
+    G4 = 1 << 32
+    size = G4 + (256 << 20)
+    n, stride = 2048, 2048
+    tmp = np.zeros(n * stride, np.uint8)
+    src = oracle.synth_batch(tmp, n, 0, stride, seed=0x5EED4444, mode=0, len_lo=64, len_hi=1500)
+    d_umem = torch.zeros(size, dtype=torch.uint8, device=dev)
+    addr = np.zeros(n, np.uint64)
+    for i in range(n):
+        t = i // 64
+        if t == 0:    # tile 0: windows in both regions
+            a = (G4 + (64 << 20) if i % 2 else 0) + i * stride
+        elif t == 1:  # tile 1: every window above 4 GiB
+            a = G4 + (128 << 20) + i * stride
+        elif i == 64 * 2 + 5:  # tile 2: one window across the 4 GiB line (16-B aligned, 32 B below it)
+            a = G4 - 32
+        else:
+            a = (16 << 20) + i * stride + (i % 3) * 16
+        addr[i] = a
+        L = min(stride, size - a)
+        d_umem[a:a + L] = torch.from_numpy(tmp[i * stride:i * stride + L]).to(dev)
+    descs = np.zeros(n, X.DESC_DTYPE)
+    descs["addr"], descs["len"] = addr, src["len"]
+    span = 1600  # >= a frame (<= 1500 B) and its window; the frames' spans do not overlap
+    spans = [(int(a), int(a) + span) for a in addr]
+    before = [d_umem[s:e].cpu().numpy().copy() for s, e in spans]
+    verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    X.echo_dev(d_umem, to_dev(descs), n, verd, recs)
+    torch.cuda.synchronize()
+    # oracle on a compact host image: each frame's span at i * span (16-B alignment kept)
+    img = np.concatenate(before + [np.zeros(64, np.uint8)])
+    hd = descs.copy()
+    hd["addr"] = np.arange(n, dtype=np.uint64) * span
+    v_ref, r_ref, _ = oracle.echo_batch(img, hd)
+    assert (v_ref == 0).all()
+    assert (verd.cpu().numpy() == v_ref).all()
+    assert (recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+    for i, (s, e) in enumerate(spans):
+        got = d_umem[s:e].cpu().numpy()
+        assert (got == img[i * span:(i + 1) * span]).all(), i
