@@ -15,12 +15,18 @@ TUNELIB  := xsknet_amd/libxsknet_amd_tune.so
 all: $(LIB) $(TUNELIB) oracle tools/echo_replay
 
 DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
+# build id of the transform kernel: a hash of the sources that define it and of the flags, reported by
+# xsk_gpu_build_id() so bench.py attaches a PMC traffic summary only to the build it was measured on
+BUILD_ID := $(shell cat $(CSRC)/xsk_echo.hip $(DEVHDR) | sha256sum | cut -c1-16)-$(shell echo '$(HIPFLAGS)' | sha256sum | cut -c1-4)
 HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_lowlat.o
 HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o
 TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(CSRC)/xsk_echo.o: $(CSRC)/xsk_echo.hip $(DEVHDR) Makefile
+	$(HIPCC) $(HIPFLAGS) -DXSK_GPU_BUILD_ID='"$(BUILD_ID)"' -c -o $@ $<
 
 $(CSRC)/tune/%.o: $(CSRC)/tune/%.hip $(DEVHDR) $(CSRC)/tune/xsk_echo_variants.h
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<

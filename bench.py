@@ -31,9 +31,9 @@ import torch  # noqa: E402
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # the transform kernel xsk_gpu_echo_dev launches for a large batch (the name rocprofv3 reports)
-KERNEL = "echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512>"
+KERNEL = "echo_round_kernel<false, false>"
 # xsk_gpu_echo_dev_opts, nonzero --opts
-WIRE_KERNEL = "echo_kernel6<4, 1, 2, 2, false, false, true, false, false, false, false, false, false, false, 0, 1, false, false, false, 0, 0, 0, 2, 1024>"
+WIRE_KERNEL = "echo_round_kernel<true, false>"
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
@@ -56,6 +56,42 @@ def log(*a):
 # Rehearsal of the N > 1 path on a one-GPU box (never used by the driver): every rank on cuda:0 and a
 # gloo process group (RCCL refuses two ranks on one device).
 SHARE_GPU = os.environ.get("XSK_BENCH_SHARE_GPU") == "1"
+
+
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpu_count(nodes=KFD_NODES, env=None):
+    """GPUs this process would see, counted WITHOUT any GPU library (the launcher parent must not touch the
+    GPU: it spawns the ranks that do).  GPU agents are the KFD topology nodes whose `gpu_id` is nonzero (CPU
+    nodes have 0); HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES narrow them as the HIP
+    runtime does (comma lists; an empty list hides every GPU).  Returns None when the topology cannot be
+    read (not a ROCm host, or sysfs hidden), so the caller can leave the decision to the ranks."""
+    env = os.environ if env is None else env
+    try:
+        names = os.listdir(nodes)
+    except OSError:
+        return None
+    n = 0
+    for name in names:
+        try:
+            gid = int(open(os.path.join(nodes, name, "gpu_id")).read().strip() or "0")
+        except (OSError, ValueError):
+            continue
+        n += 1 if gid != 0 else 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is None:
+            continue
+        ids = [x.strip() for x in v.split(",") if x.strip()]
+        # numeric ids past the last GPU select nothing (HIP stops at the first invalid one)
+        ok = 0
+        for x in ids:
+            if x.isdigit() and int(x) >= n:
+                break
+            ok += 1
+        n = min(n, ok)
+    return n
 
 
 def launch_ranks(gpus):
@@ -206,32 +242,25 @@ def _cpu_model():
     return "unknown"
 
 
-def traffic_from_profiles(cfg, kernel):
+def traffic_from_profiles(cfg, kernel, build_id, path=None):
     """PMC-derived HBM bytes per launch from the committed rocprofv3 --pmc summary of this config
-    (tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled on gfx950),
-    or None when there is none for the kernel that ran."""
-    p = os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
-    env = os.environ.get("XSK_TRAFFIC_JSON")  # a fresh summary of this build (tools/gpu_full.sh)
-    if env and os.path.basename(env) == os.path.basename(p):
-        p = env
+    (tools/pmc_summary.py: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled on gfx950).
+    Returns (bytes or None, source): the summary counts only when it names exactly the kernel that ran
+    (full demangled template string) AND the build id of the running library (xsk_gpu_build_id(): a hash
+    of the kernel sources and flags), so a stale summary is never attached to a different kernel."""
+    p = path or os.path.join(ROOT, "profiles", f"traffic_{cfg}.json")
+    rel = os.path.relpath(p, ROOT)
     try:
         d = json.load(open(p))
     except (OSError, ValueError):
-        return None
-    return d.get("hbm_bytes_per_launch") if d.get("kernel") and _kname(d["kernel"]) == _kname(kernel) else None
-
-
-def _kname(k):
-    """A kernel's demangled template name without trailing default-valued arguments (false / 0), so that
-    adding a defaulted template parameter does not orphan the committed profiles of the same kernel."""
-    k = k.strip()
-    if not k.endswith(">") or "<" not in k:
-        return k
-    base, args = k[:-1].split("<", 1)
-    a = [x.strip() for x in args.split(",")]
-    while a and a[-1] in ("false", "0", "1024"):  # 1024: HEAVY's default (xsk_echo_device.h kHeavyLen)
-        a.pop()
-    return base + "<" + ", ".join(a) + ">"
+        return None, f"none: no summary at {rel}"
+    if d.get("kernel") != kernel:
+        return None, f"none: {rel} profiles kernel {d.get('kernel')!r}, not the one that ran"
+    if not build_id or d.get("build_id") != build_id:
+        return None, f"none: {rel} is of build {d.get('build_id')!r}, the running library is {build_id!r}"
+    b = d.get("hbm_bytes_per_launch")
+    return (int(b), f"{rel} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this build)") if b else \
+        (None, f"none: {rel} has no byte count")
 
 
 def host_inclusive(cfg, dev_index):
@@ -269,6 +298,18 @@ def host_inclusive(cfg, dev_index):
     return out
 
 
+def pool_plan(n, stride, free, warmup, steps, cap=0):
+    """Batches in the pool (each: n frames at `stride` + n descriptors) and whether a step must re-arm its
+    batch inside the timed loop: one fresh batch per step while W + K batches fit in 85 % of the free HBM
+    (less one batch of headroom for the outputs), else the largest pool that does, re-armed from its own
+    verdicts when reused.  c5 per rank: 64 M / N frames at 2 KiB = 128 GiB / N per batch."""
+    per_batch = n * stride + n * 16
+    pool = max(1, min(warmup + steps, int(free * 0.85) // per_batch - 1))
+    if cap:
+        pool = min(pool, cap)
+    return pool, pool < warmup + steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -289,9 +330,10 @@ def main():
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # counting devices does not initialise the GPU on this image; nothing else here touches it
-        if not SHARE_GPU and torch.cuda.device_count() < args.gpus:
-            raise SystemExit(f"--gpus {args.gpus} but {torch.cuda.device_count()} GPU(s) visible "
+        # the parent never touches a GPU library: it counts GPUs in the KFD topology and spawns the ranks
+        ngpu = None if SHARE_GPU else kfd_gpu_count()
+        if ngpu is not None and ngpu < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but {ngpu} GPU(s) visible "
                              "(XSK_BENCH_SHARE_GPU=1 rehearses N ranks on one GPU)")
         sys.exit(launch_ranks(args.gpus))
 
@@ -314,11 +356,7 @@ def main():
     # ---- batch pool: one fresh batch per step (generated on the GPU, bit-identical to the oracle) ----
     batch_bytes = n * stride
     free, _ = torch.cuda.mem_get_info(dev)
-    per_batch = batch_bytes + n * 16
-    pool = max(1, min(W + K, int(free * 0.85) // per_batch - 1))
-    if args.pool_cap:
-        pool = min(pool, args.pool_cap)
-    rearm_in_loop = pool < W + K
+    pool, rearm_in_loop = pool_plan(n, stride, free, W, K, args.pool_cap)
     log(f"[rank {rank}] {desc}; world {world}; pool {pool} batches of {batch_bytes / 2**30:.2f} GiB"
         + (" (re-arm inside timed loop)" if rearm_in_loop else ""))
     umems, descss = [], []
@@ -420,11 +458,23 @@ def main():
     wall_max, ev_max = allreduce([wall, ev_ms], op_max, world, dev)
     ok_all, frames_all, bytes_all = allreduce([1.0 if ok else 0.0, float(K * n), float(K * frame_bytes)], op_sum,
                                               world, dev)
+    # every rank's own figures, gathered into rank 0's line (slot r of a zeroed vector, summed)
+    kern_avg_ms = kern_ms / max(launches, 1)
+    achieved = frame_bytes / (kern_avg_ms / 1e3) / 1e9
+    mine = [0.0] * (5 * world)
+    mine[5 * rank:5 * rank + 5] = [kern_avg_ms * 1e3, achieved, wall, float(K * n), float(local)]
+    per_rank_flat = allreduce(mine, op_sum, world, dev)
 
     if rank == 0:
         value = frames_all / wall_max / 1e6
-        kern_avg_ms = kern_ms / max(launches, 1)
-        achieved = frame_bytes / (kern_avg_ms / 1e3) / 1e9
+        per_rank = [{"rank": r, "device": int(per_rank_flat[5 * r + 4]),
+                     "kernel_avg_us": round(per_rank_flat[5 * r], 2),
+                     "achieved_gbs": round(per_rank_flat[5 * r + 1], 1),
+                     "frac": round(per_rank_flat[5 * r + 1] / HBM_PEAK_GBS, 4),
+                     "wall_ms": round(per_rank_flat[5 * r + 2] * 1e3, 3),
+                     "frames": int(per_rank_flat[5 * r + 3])} for r in range(world)]
+        traffic, traffic_src = (None, "none: wire mode is not profiled") if args.opts else \
+            traffic_from_profiles(args.config, kernel, X.build_id())
         res = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -448,10 +498,13 @@ def main():
             **({"ab_variant": args.variant, "note": "A/B timing of a tuning variant, not the shipped kernel"}
                if args.variant >= 0 else {}),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic_from_profiles(args.config, kernel) if args.opts == 0 else None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "build_id": X.build_id(),
                          "kernel": kernel, "kernel_avg_us": round(kern_avg_ms * 1e3, 2), "kernel_timer": timer_src,
                          "algorithmic_bytes_per_launch": frame_bytes,
-                         "read_ceiling_gbs": round(read_ceiling, 1)},
+                         "read_ceiling_gbs": round(read_ceiling, 1),
+                         "note": "rank 0's kernel; every rank's in per_rank"},
+            "per_rank": per_rank,
             "event_ms_per_step": round(ev_max / K, 4),
         }
         if world == 1 and not args.no_cpu:

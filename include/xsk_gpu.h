@@ -358,6 +358,11 @@ int xsk_gpu_timing_read(double* total_ms, uint64_t* launches);
 int xsk_gpu_abi_version(void);
 const char* xsk_gpu_last_error(void);
 
+/* Build id of the transform kernel in this library: a hash of the sources that define it and of the
+ * compiler flags (static string).  Profiles record it so that measured counters are only ever
+ * attributed to the build they were taken on. */
+const char* xsk_gpu_build_id(void);
+
 #ifdef __cplusplus
 }
 #endif

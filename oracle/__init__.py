@@ -60,6 +60,7 @@ def lib() -> C.CDLL:
             "oracle_echo_batch": ([_P, C.c_uint64, _P, C.c_uint32, _P, _P, _P], None),
             "oracle_echo_batch_mt": ([_P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, C.c_int], None),
             "oracle_echo_batch_opts": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P], None),
+            "oracle_echo_batch_opts_mt": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, C.c_int], None),
             "oracle_echo_batch_hdr": ([_P, _P, C.c_uint32, _P, _P], None),
             "oracle_echo_batch_hdr_mt": ([_P, _P, C.c_uint32, _P, _P, C.c_int], None),
             "oracle_synth_frame": ([C.c_uint64, C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, _P, C.c_uint32],
@@ -114,15 +115,19 @@ def echo_batch(umem: np.ndarray, descs: np.ndarray, threads: int = 1):
     return verdicts, recs, stats[0]
 
 
-def echo_batch_opts(umem: np.ndarray, descs: np.ndarray, opts: int):
+def echo_batch_opts(umem: np.ndarray, descs: np.ndarray, opts: int, threads: int = 1):
     """xsk_gpu_echo_dev_opts' contract (wire-format widening for opts != 0) on host arrays."""
     n = len(descs)
     descs = np.ascontiguousarray(descs, DESC_DTYPE)
     verdicts = np.zeros(n, np.uint8)
     recs = np.zeros(n, REC_DTYPE)
     stats = np.zeros(1, STATS_DTYPE)
-    lib().oracle_echo_batch_opts(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, opts, verdicts.ctypes.data,
-                                 recs.ctypes.data, stats.ctypes.data)
+    if threads > 1:
+        lib().oracle_echo_batch_opts_mt(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, opts,
+                                        verdicts.ctypes.data, recs.ctypes.data, stats.ctypes.data, threads)
+    else:
+        lib().oracle_echo_batch_opts(umem.ctypes.data, umem.nbytes, descs.ctypes.data, n, opts, verdicts.ctypes.data,
+                                     recs.ctypes.data, stats.ctypes.data)
     return verdicts, recs, stats[0]
 
 

@@ -167,24 +167,52 @@ struct mt_job {
     uint8_t* verdicts;
     struct xsk_gpu_rec* recs;
     struct xsk_gpu_stats st;
-    int hdr_only;
+    int kind;      /* 0 full contract, 1 header-only, 2 wire mode (opts) */
+    uint32_t opts;
 };
 
 static void* mt_worker(void* arg) {
     struct mt_job* j = (struct mt_job*)arg;
-    if (j->hdr_only)
+    if (j->kind == 1)
         oracle_echo_batch_hdr(j->umem, j->descs, j->n, j->verdicts, &j->st);
+    else if (j->kind == 2)
+        oracle_echo_batch_opts(j->umem, j->umem_size, j->descs, j->n, j->opts, j->verdicts, j->recs, &j->st);
     else
         oracle_echo_batch(j->umem, j->umem_size, j->descs, j->n, j->verdicts, j->recs, &j->st);
     return NULL;
 }
 
+/* Run jobs[0..threads) on `threads` threads: job 0 on the caller's thread, and any job whose thread cannot be
+ * created inline on the caller's thread too; only the threads that started are joined. */
+static void run_jobs(void* jobs, size_t job_size, int threads, void* (*fn)(void*)) {
+    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof *tids);
+    int* started = (int*)calloc((size_t)threads, sizeof *started);
+    for (int t = 1; t < threads; t++)
+        started[t] = tids && started && pthread_create(&tids[t], NULL, fn, (char*)jobs + (size_t)t * job_size) == 0;
+    for (int t = 0; t < threads; t++)
+        if (!started || !started[t]) fn((char*)jobs + (size_t)t * job_size);
+    for (int t = 1; t < threads; t++)
+        if (started && started[t]) pthread_join(tids[t], NULL);
+    free(tids);
+    free(started);
+}
+
 static void run_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
-                   struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats, int threads, int hdr_only) {
+                   struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats, int threads, int kind, uint32_t opts) {
     if (threads < 1) threads = 1;
     if ((uint32_t)threads > n) threads = n ? (int)n : 1;
     struct mt_job* jobs = (struct mt_job*)calloc((size_t)threads, sizeof *jobs);
-    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof *tids);
+    if (!jobs) { /* no memory for the job table: one job on this thread */
+        struct mt_job one = {umem, umem_size, descs, n, verdicts, recs, {0, 0, 0, 0, 0}, kind, opts};
+        mt_worker(&one);
+        if (stats) {
+            stats->rx_packets += one.st.rx_packets;
+            stats->rx_bytes += one.st.rx_bytes;
+            stats->tx_packets += one.st.tx_packets;
+            stats->tx_bytes += one.st.tx_bytes;
+        }
+        return;
+    }
     uint32_t start = 0;
     for (int t = 0; t < threads; t++) {
         const uint32_t cnt = n / threads + ((uint32_t)t < n % threads ? 1 : 0);
@@ -194,12 +222,11 @@ static void run_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc*
         jobs[t].n = cnt;
         jobs[t].verdicts = verdicts ? verdicts + start : NULL;
         jobs[t].recs = recs ? recs + start : NULL;
-        jobs[t].hdr_only = hdr_only;
+        jobs[t].kind = kind;
+        jobs[t].opts = opts;
         start += cnt;
-        if (t > 0) pthread_create(&tids[t], NULL, mt_worker, &jobs[t]);
     }
-    mt_worker(&jobs[0]);
-    for (int t = 1; t < threads; t++) pthread_join(tids[t], NULL);
+    run_jobs(jobs, sizeof *jobs, threads, mt_worker);
     if (stats) {
         for (int t = 0; t < threads; t++) {
             stats->rx_packets += jobs[t].st.rx_packets;
@@ -209,17 +236,16 @@ static void run_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc*
         }
     }
     free(jobs);
-    free(tids);
 }
 
 void oracle_echo_batch_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
                           uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats, int threads) {
-    run_mt(umem, umem_size, descs, n, verdicts, recs, stats, threads, 0);
+    run_mt(umem, umem_size, descs, n, verdicts, recs, stats, threads, 0, 0);
 }
 
 void oracle_echo_batch_hdr_mt(uint8_t* umem, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                               struct xsk_gpu_stats* stats, int threads) {
-    run_mt(umem, 0, descs, n, verdicts, NULL, stats, threads, 1);
+    run_mt(umem, 0, descs, n, verdicts, NULL, stats, threads, 1, 0);
 }
 
 /* ---------------------------------------------------------------------------------------------- */
@@ -329,12 +355,8 @@ int oracle_synth_batch_mt(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc
     if (threads < 1) threads = 1;
     if ((uint32_t)threads > n) threads = n ? (int)n : 1;
     struct synth_job* jobs = (struct synth_job*)calloc((size_t)threads, sizeof *jobs);
-    pthread_t* tids = (pthread_t*)calloc((size_t)threads, sizeof *tids);
-    if (!jobs || !tids) {
-        free(jobs);
-        free(tids);
-        return -1;
-    }
+    if (!jobs)
+        return oracle_synth_batch(umem, umem_size, descs, n, base_off, stride, seed, first, step, mode, len_lo, len_hi);
     uint32_t start = 0;
     for (int t = 0; t < threads; t++) {
         const uint32_t cnt = n / threads + ((uint32_t)t < n % threads ? 1 : 0);
@@ -342,15 +364,12 @@ int oracle_synth_batch_mt(uint8_t* umem, uint64_t umem_size, struct xsk_gpu_desc
                                len_hi, 0};
         jobs[t] = jb;
         start += cnt;
-        if (t > 0) pthread_create(&tids[t], NULL, synth_worker, &jobs[t]);
     }
-    synth_worker(&jobs[0]);
+    run_jobs(jobs, sizeof *jobs, threads, synth_worker);
     int rc = 0;
-    for (int t = 1; t < threads; t++) pthread_join(tids[t], NULL);
     for (int t = 0; t < threads; t++)
         if (jobs[t].rc) rc = jobs[t].rc;
     free(jobs);
-    free(tids);
     return rc;
 }
 
@@ -480,6 +499,13 @@ void oracle_echo_batch_opts(uint8_t* umem, uint64_t umem_size, const struct xsk_
         stats->tx_packets += txp;
         stats->tx_bytes += txb;
     }
+}
+
+/* oracle_echo_batch_opts over `threads` pthreads (contiguous descriptor ranges; frames never overlap). */
+void oracle_echo_batch_opts_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
+                               uint32_t opts, uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats,
+                               int threads) {
+    run_mt(umem, umem_size, descs, n, verdicts, recs, stats, threads, 2, opts);
 }
 
 /* ---------------------------------------------------------------------------------------------- */

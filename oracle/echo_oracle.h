@@ -44,6 +44,10 @@ void oracle_echo_batch_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gp
  * widening of include/xsk_gpu.h (XSK_GPU_OPT_*), build-added. */
 void oracle_echo_batch_opts(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
                             uint32_t opts, uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+/* oracle_echo_batch_opts over `threads` pthreads (same bytes, verdicts, records and counters). */
+void oracle_echo_batch_opts_mt(uint8_t* umem, uint64_t umem_size, const struct xsk_gpu_desc* descs, uint32_t n,
+                               uint32_t opts, uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats,
+                               int threads);
 
 /* Reference-equivalent work only (gates + rewrite + counters; no full-payload sums, no records):
  * the CPU-baseline variant that does exactly what process_packet does. */

@@ -150,7 +150,8 @@ def test_tuning_code_is_not_in_the_product_library():
     # the product exports the C ABI, plus the CU count the tuning library links against and a
     # diagnostics hook of the LOWLAT channel (tools/echo_replay)
     exported = set(re.findall(r"\bT (\w+)", prod))
-    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu", "xsk_gpu__lowlat_trace"}, \
+    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu", "xsk_gpu__lowlat_trace",
+                                                    "xsk_gpu__echo_dev_grid"}, \
         exported - set(declared_functions())
     tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
                           check=True).stdout

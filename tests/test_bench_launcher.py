@@ -31,7 +31,10 @@ def test_launcher_spawns_n_ranks(monkeypatch):
         raise AssertionError("the launcher must not load the HIP library")
 
     monkeypatch.setattr(xsknet_amd, "lib", no_gpu)
-    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    # the parent counts GPUs in the KFD topology only: every torch / HIP device query must stay untouched
+    for fn in ("device_count", "is_available", "init", "set_device", "mem_get_info", "synchronize"):
+        monkeypatch.setattr(bench.torch.cuda, fn, no_gpu)
+    monkeypatch.setattr(bench, "kfd_gpu_count", lambda *a, **k: 8)
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5", "--config", "c5"])
     with pytest.raises(SystemExit) as e:
@@ -90,8 +93,88 @@ def test_launcher_refuses_more_ranks_than_gpus(monkeypatch):
     bench = _bench()
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(bench, "SHARE_GPU", False)
-    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setattr(bench, "kfd_gpu_count", lambda *a, **k: 1)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: (_ for _ in ()).throw(AssertionError("GPU query")))
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert "1 GPU(s) visible" in str(e.value)
+
+
+def test_launcher_without_kfd_leaves_it_to_the_ranks(monkeypatch):
+    """No readable KFD topology: the parent launches anyway (a rank without a GPU fails loudly itself)."""
+    bench = _bench()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "SHARE_GPU", False)
+    monkeypatch.setattr(bench, "KFD_NODES", "/nonexistent/kfd/nodes")
+    monkeypatch.setattr(bench, "kfd_gpu_count", lambda *a, **k: None)
+    monkeypatch.setattr(bench, "launch_ranks", lambda g: 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0
+
+
+def _fake_kfd(root, gpu_ids):
+    for i, g in enumerate(gpu_ids):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "gpu_id").write_text(f"{g}\n")
+        (d / "properties").write_text(f"cpu_cores_count {0 if g else 64}\nsimd_count {0 if not g else 1024}\n")
+    return str(root)
+
+
+def test_kfd_parser_counts_gpu_nodes(tmp_path):
+    """The KFD topology of an 8-GPU node: 2 CPU nodes (gpu_id 0) + 8 GPU nodes; visibility lists narrow it."""
+    bench = _bench()
+    nodes = _fake_kfd(tmp_path / "nodes", [0, 0, 41234, 52345, 63456, 7456, 8567, 9678, 10789, 11890])
+    assert bench.kfd_gpu_count(nodes, env={}) == 8
+    assert bench.kfd_gpu_count(nodes, env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
+    assert bench.kfd_gpu_count(nodes, env={"ROCR_VISIBLE_DEVICES": "3"}) == 1
+    assert bench.kfd_gpu_count(nodes, env={"CUDA_VISIBLE_DEVICES": ""}) == 0
+    assert bench.kfd_gpu_count(nodes, env={"HIP_VISIBLE_DEVICES": "0,9,1"}) == 1  # stops at the invalid id
+    assert bench.kfd_gpu_count(nodes, env={"HIP_VISIBLE_DEVICES": "0,1,2,3", "ROCR_VISIBLE_DEVICES": "0,1"}) == 2
+    # a node without gpu_id (a partially populated topology) is skipped
+    os = __import__("os")
+    os.remove(os.path.join(nodes, "2", "gpu_id"))
+    assert bench.kfd_gpu_count(nodes, env={}) == 7
+    assert bench.kfd_gpu_count(str(tmp_path / "missing"), env={}) is None
+
+
+def test_traffic_provenance(tmp_path):
+    """roofline.traffic is attached only when the summary names the kernel that ran AND the running build."""
+    import json
+    bench = _bench()
+    k = bench.KERNEL
+    p = tmp_path / "traffic_c3.json"
+    p.write_text(json.dumps({"kernel": k, "build_id": "abc", "hbm_bytes_per_launch": 1714382400}))
+    assert bench.traffic_from_profiles("c3", k, "abc", str(p))[0] == 1714382400
+    t, src = bench.traffic_from_profiles("c3", k, "other", str(p))
+    assert t is None and "build" in src
+    t, src = bench.traffic_from_profiles("c3", k + " ", "abc", str(p))
+    assert t is None and "kernel" in src
+    p.write_text(json.dumps({"kernel": k, "hbm_bytes_per_launch": 1}))  # no build id recorded
+    assert bench.traffic_from_profiles("c3", k, "abc", str(p))[0] is None
+    assert bench.traffic_from_profiles("c3", k, "abc", str(tmp_path / "none.json"))[0] is None
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_c5_pool_plan(world):
+    """c5 splits 64 M x 1500-B frames (2 KiB stride) over the ranks: the per-rank batch, the pool that fits a
+    288 GB MI355X (about 280 GiB free after the runtime) and the re-arm decision for the driver's K=20, W=5."""
+    bench = _bench()
+    n_total, lo, hi, stride = bench.CONFIGS["c5"][:4]
+    assert n_total % world == 0
+    n = n_total // world
+    free = 280 * 2**30
+    pool, rearm = bench.pool_plan(n, stride, free, 5, 20)
+    per = n * stride + n * 16
+    assert pool >= 1 and (pool + 1) * per <= free * 0.85 or pool == 1
+    assert rearm == (pool < 25)
+    # the pool's outputs (verdicts per pooled batch when re-arming, records, stats) still fit beside it
+    outputs = (pool if rearm else 1) * n + n * 16 + 40
+    assert pool * per + outputs < free
+    if world == 1:
+        assert pool == 1 and rearm  # 128 GiB: one batch, re-armed every step
+    if world == 8:
+        assert pool >= 10  # 16 GiB batches

@@ -133,36 +133,64 @@ def test_wire_bad_options_rejected():
         X.echo_dev(d, d, 1, opts=8)
 
 
-def test_wire_full_size_c3():
-    """1 M x 1500-B valid echo requests at a 4 KiB stride with every option on: all replied, both
-    checksums verify, counters exact, 512 sampled frames byte-exact against the oracle."""
+def wire_full_batch_parity(n, lo, hi, stride, seed, opts, mode=0, chunk=1 << 19):
+    """n frames generated on the GPU, transformed in wire mode by ONE xsk_gpu_echo_dev_opts call; every byte of
+    the slab, every verdict, record and counter against oracle_echo_batch_opts on a host image regenerated by
+    oracle.synth_batch chunk by chunk (bounded host memory)."""
+    from tests.test_gpu_parity import _threads
     dev = _dev()
-    n, stride, seed = 1 << 20, 4096, 0x5EED0003
     d_umem = torch.zeros(n * stride, dtype=torch.uint8, device=dev)
     d_descs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    X.synth_dev(d_umem, d_descs, n, 0, stride, seed, 0, 1, 0, 1500, 1500)
-    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    X.synth_dev(d_umem, d_descs, n, 0, stride, seed, 0, 1, mode, lo, hi)
+    d_verd = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
     d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
     d_stats = torch.zeros(40, dtype=torch.uint8, device=dev)
     ws = torch.zeros(X.workspace_size(0, n), dtype=torch.uint8, device=dev)
-    X.echo_dev(d_umem, d_descs, n, d_verd, d_recs, d_stats, ws, opts=X.OPT_ALL)
+    X.echo_dev(d_umem, d_descs, n, d_verd, d_recs, d_stats, ws, opts=opts)
     torch.cuda.synchronize()
+    verdicts = d_verd.cpu().numpy()
     recs = d_recs.cpu().numpy().view(X.REC_DTYPE)
-    stats = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
-    assert (d_verd.cpu().numpy() == 0).all()
-    assert (recs["flags"] == 3).all()
-    assert int(stats["tx_packets"]) == n and int(stats["tx_bytes"]) == n * 1500
-    rng = np.random.default_rng(3)
-    idx = np.sort(rng.choice(n, 512, replace=False))
-    got = d_umem.view(-1, stride)[torch.from_numpy(idx).to(dev)].cpu().numpy()
-    for k, j in enumerate(idx):
-        L, buf = oracle.synth_frame(seed, int(j), 0, 1500, 1500, cap=stride)
-        frame = buf[:stride].copy()
-        d1 = np.zeros(1, oracle.DESC_DTYPE)
-        d1[0] = (0, L, 0)
-        v, r, _ = oracle.echo_batch_opts(frame, d1, X.OPT_ALL)
-        assert v[0] == 0 and r[0] == recs[j]
-        assert (got[k] == frame).all(), j
+    descs_all = d_descs.cpu().numpy().view(X.DESC_DTYPE)
+    tot = {k: 0 for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")}
+    th = _threads()
+    for j0 in range(0, n, chunk):
+        m = min(chunk, n - j0)
+        host = np.zeros(m * stride, np.uint8)
+        descs = oracle.synth_batch(host, m, 0, stride, seed, j0, 1, mode, lo, hi, threads=th)
+        assert (descs["len"] == descs_all["len"][j0:j0 + m]).all()
+        v_ref, r_ref, s_ref = oracle.echo_batch_opts(host, descs, opts, threads=th)
+        got = d_umem[j0 * stride:(j0 + m) * stride].cpu().numpy()
+        diff = np.nonzero(got != host)[0]
+        assert len(diff) == 0, f"frames from {j0}: {len(diff)} bytes differ, first at {diff[:8]}"
+        bad = np.nonzero(verdicts[j0:j0 + m] != v_ref)[0]
+        assert len(bad) == 0, (j0 + bad[:5])
+        bad = np.nonzero(recs[j0:j0 + m] != r_ref)[0]
+        assert len(bad) == 0, (j0 + bad[:5])
+        for k in tot:
+            tot[k] += int(s_ref[k])
+        del host, got
+    st = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
+    for k in tot:
+        assert int(st[k]) == tot[k], k
+    return verdicts, recs
+
+
+@pytest.mark.parametrize("cfg", ["c2_64", "c3_1500", "c4_mixed"])
+def test_wire_full_size_configs(cfg):
+    """BASELINE configs 2-4 at full size (1 M frames, one call) in wire mode with every option on: every frame
+    byte-exact vs the oracle (the widening replaces the fixed offsets of xsk_receive.c:120-121)."""
+    lo, hi, stride = {"c2_64": (64, 64, 64), "c3_1500": (1500, 1500, 4096), "c4_mixed": (64, 1500, 2048)}[cfg]
+    seed = 0x5EED0000 + {"c2_64": 2, "c3_1500": 3, "c4_mixed": 4}[cfg]
+    v, r = wire_full_batch_parity(1 << 20, lo, hi, stride, seed, X.OPT_ALL)
+    assert (v == 0).all() and ((r["flags"] & 3) == 3).all()
+
+
+@pytest.mark.parametrize("opts", [1, 2, 7])
+def test_wire_full_size_mixed_traffic(opts):
+    """1 M frames of every negative / edge case (synth mode 1) at a 2 KiB stride in wire mode, every frame vs
+    the oracle."""
+    v, _ = wire_full_batch_parity(1 << 20, 20, 1500, 2048, 0x5EED0044 + opts, opts, mode=1)
+    assert len(np.unique(v)) >= 5
 
 
 def test_wire_multi_round_mixed():
@@ -190,42 +218,3 @@ def test_wire_multi_round_mixed():
         descs[i] = (a, L, 0)
     v = check(umem, descs, X.OPT_ALL)
     assert (v == X.DROP_BAD_IP).any() and (v == 0).any()
-
-
-@pytest.mark.parametrize("variant", [160, 161, 162])
-@pytest.mark.parametrize("grid", [1, 3])
-def test_wire_tuning_variants(variant, grid):
-    """The wire-mode round kernel from the tuning library (160: as shipped, 161: write-through write phases)
-    on mixed wire traffic, shares of many rounds (1-3 workgroups), every option on, against the oracle."""
-    from tests.wire_frames import random_frame
-    dev = _dev()
-    L = X.tune_lib()
-    rng = np.random.default_rng(4242)
-    pool = []
-    while len(pool) < 512:
-        f, ln = random_frame(rng)
-        pool.append((np.frombuffer(f, np.uint8), ln))
-    n, stride = 20_000, 2048
-    umem = rng.integers(0, 256, n * stride + 256, dtype=np.uint8)
-    descs = np.zeros(n, oracle.DESC_DTYPE)
-    for i in range(n):
-        fr, ln = pool[(i * 7919) % len(pool)]
-        a = i * stride + (i % 16)
-        umem[a:a + fr.size] = fr
-        descs[i] = (a, ln, 0)
-    ref = umem.copy()
-    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
-    d_umem, d_descs = to_dev(umem), to_dev(np.ascontiguousarray(descs, X.DESC_DTYPE))
-    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
-    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
-    rc = L.xsk_gpu__echo_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
-                                 d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
-                                 torch.cuda.current_stream().cuda_stream)
-    assert rc == 0
-    torch.cuda.synchronize()
-    assert (d_verd.cpu().numpy() == v_ref).all()
-    assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
-    assert (d_umem.cpu().numpy() == ref).all()
-    part = ws[:grid * 32].cpu().numpy().view(np.uint64).reshape(grid, 4).sum(axis=0)
-    assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]

@@ -151,6 +151,23 @@ def test_mt_matches_single_thread():
     v1, r1, s1 = oracle.echo_batch(u1, descs)
     v2, r2, s2 = oracle.echo_batch(u2, descs, threads=4)
     assert (v1 == v2).all() and (r1 == r2).all() and s1 == s2 and (u1 == u2).all()
+    # more threads than frames, and the synth side
+    u3 = np.zeros(n * 256, np.uint8)
+    d3 = oracle.synth_batch(u3, n, 0, 256, seed=9, mode=1, len_lo=20, len_hi=200, threads=7)
+    assert (d3 == descs).all()
+    v4, r4, s4 = oracle.echo_batch(u3[:5 * 256].copy(), d3[:5], threads=16)
+    v5, r5, s5 = oracle.echo_batch(u3[:5 * 256].copy(), d3[:5])
+    assert (v4 == v5).all() and (r4 == r5).all() and s4 == s5
+
+
+@pytest.mark.parametrize("opts", [1, 2, 7])
+def test_wire_mt_matches_single_thread(opts):
+    from tests.wire_frames import mixed_batch
+    u1, descs = mixed_batch(3000, 2048, seed=31 + opts, offsets=True)
+    u2 = u1.copy()
+    v1, r1, s1 = oracle.echo_batch_opts(u1, descs, opts)
+    v2, r2, s2 = oracle.echo_batch_opts(u2, descs, opts, threads=5)
+    assert (v1 == v2).all() and (r1 == r2).all() and s1 == s2 and (u1 == u2).all()
 
 
 def test_xdp_classify_golden():

@@ -18,7 +18,7 @@ import sys
 
 def main():
     d, out = sys.argv[1], sys.argv[2]
-    ksub = sys.argv[3] if len(sys.argv) > 3 else "echo_kernel6"
+    ksub = sys.argv[3] if len(sys.argv) > 3 else "echo_round_kernel"
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if ksub in r["Kernel_Name"]]
     by = {}
@@ -26,7 +26,7 @@ def main():
         by.setdefault(r["Counter_Name"], {}).setdefault(r["Dispatch_Id"], 0.0)
         by[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     med = {c: statistics.median(v.values()) for c, v in by.items()}
-    m = re.search(r"echo_kernel\d<[^>]*>", rows[0]["Kernel_Name"])
+    m = re.search(r"echo_\w*kernel\d*<[^>]*>", rows[0]["Kernel_Name"])
     res = {"kernel": m.group(0) if m else rows[0]["Kernel_Name"][:120],
            "launches": len(next(iter(by.values()))), "median_per_launch": med}
     if "SQ_INSTS_VALU" in med:

@@ -19,7 +19,7 @@ from typing import Optional
 import numpy as np
 
 __all__ = [
-    "LIB_PATH", "lib", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
+    "LIB_PATH", "lib", "build_id", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
     "MODE_ZEROCOPY", "MODE_STAGED", "MODE_LOWLAT", "LOWLAT_MAX", "MultiContext", "tune_lib", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
@@ -92,6 +92,7 @@ _P = C.c_void_p
 _SIGS = {
     "xsk_gpu_abi_version": ([], C.c_int),
     "xsk_gpu_last_error": ([], C.c_char_p),
+    "xsk_gpu_build_id": ([], C.c_char_p),
     "xsk_gpu_workspace_size": ([C.c_int, C.c_uint32], C.c_size_t),
     "xsk_gpu_echo_dev": ([_P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P, _P], C.c_int),
     "xsk_gpu_echo_dev_opts": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P], C.c_int),
@@ -114,6 +115,8 @@ _SIGS = {
     "xsk_gpu_multi_process": ([_P, _P, C.c_uint32, _P, _P, _P], C.c_int),
     "xsk_gpu_multi_set_options": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu_multi_fini": ([_P], None),
+    # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
+    "xsk_gpu__echo_dev_grid": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32], C.c_int),
 }
 _TUNE_SIGS = {
     "xsk_gpu__echo_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
@@ -172,14 +175,25 @@ def _stream_ptr(stream) -> Optional[int]:
     return getattr(stream, "cuda_stream", stream)
 
 
+def build_id() -> str:
+    """xsk_gpu_build_id(): hash of the transform kernel's sources and flags in the loaded library."""
+    return lib().xsk_gpu_build_id().decode()
+
+
 def workspace_size(device: int, n: int) -> int:
     return int(lib().xsk_gpu_workspace_size(device, n))
 
 
 def echo_dev(umem, descs, n: int, verdicts=None, recs=None, stats=None, workspace=None, stream=None,
-             opts: int = 0) -> None:
+             opts: int = 0, grid: int = 0) -> None:
     """xsk_gpu_echo_dev (opts == 0) / xsk_gpu_echo_dev_opts on torch device tensors (uint8 umem,
-    uint8/int64 views of the structs)."""
+    uint8/int64 views of the structs).  grid != 0: the same product kernel with that many workgroups for a
+    large batch (internal hook xsk_gpu__echo_dev_grid, tests only)."""
+    if grid:
+        _check("xsk_gpu__echo_dev_grid", lib().xsk_gpu__echo_dev_grid(
+            _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, opts, _ptr(verdicts), _ptr(recs),
+            _ptr(stats), _ptr(workspace), _stream_ptr(stream), grid))
+        return
     if opts:
         _check("xsk_gpu_echo_dev_opts", lib().xsk_gpu_echo_dev_opts(
             _ptr(umem), umem.numel() * umem.element_size(), _ptr(descs), n, opts, _ptr(verdicts), _ptr(recs),

@@ -4,7 +4,7 @@
 // DESIGN.md §3 has their measurements.
 #pragma once
 
-#include "../xsk_echo_device.h"
+#include "xsk_echo_lab.h"
 
 namespace xskgpu {
 namespace {

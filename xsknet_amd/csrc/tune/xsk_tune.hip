@@ -10,7 +10,7 @@
 //   50-54 the shipped row-streaming kernel at other U (loads in flight) / occupancy settings
 #include <errno.h>
 
-#include "../xsk_echo_device.h"
+#include "xsk_echo_lab.h"
 #include "../xsk_hip_util.h"
 #include "xsk_echo_variants.h"
 

@@ -19,7 +19,7 @@
 // inside the first 64 bytes leave as whole 64-B sectors; every other reply is patched byte-exact.
 #include <errno.h>
 
-#include "../xsk_echo_device.h"
+#include "xsk_echo_lab.h"
 #include "../xsk_hip_util.h"
 
 using namespace xskgpu;

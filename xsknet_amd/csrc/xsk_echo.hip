@@ -108,6 +108,10 @@ int xsk_gpu__hip_fail(hipError_t e) {
 }
 
 int xsk_gpu_abi_version(void) { return XSK_GPU_ABI_VERSION; }
+#ifndef XSK_GPU_BUILD_ID
+#error "XSK_GPU_BUILD_ID is set by the Makefile (hash of the kernel sources and flags)"
+#endif
+const char* xsk_gpu_build_id(void) { return XSK_GPU_BUILD_ID; }
 const char* xsk_gpu_last_error(void) { return g_last_error; }
 
 size_t xsk_gpu_workspace_size(int device, uint32_t n) {
@@ -138,7 +142,7 @@ uint32_t xsk_gpu__num_cu(int device) {
 // that a one-workgroup fold launch adds.
 static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t opts,
                        uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
-                       void* d_workspace, void* stream, int hoststats, uint32_t tile) {
+                       void* d_workspace, void* stream, int hoststats, uint32_t tile, uint32_t grid_force = 0) {
     if (opts & ~XSK_GPU_OPT_ALL) return -EINVAL;
     if (n == 0) return 0;
     if (n > XSK_GPU_MAX_BATCH) return -EINVAL;
@@ -163,7 +167,7 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
         grid = 1;
         tiles_per_wg = (n + tl - 1) / tl;
     } else {
-        echo6_geometry(n, ncu, &grid, &tiles_per_wg);
+        echo6_geometry(n, grid_force ? grid_force : ncu, &grid, &tiles_per_wg);
     }
     const hipStream_t s = (hipStream_t)stream;
     EchoArgs args;
@@ -190,20 +194,13 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     }
     const int slot = timer_begin(device, s);
     if (opts == 0 && !small)
-        echo_kernel6<kShip6U, kShip6TPW, kShip6Sync, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2,
-                     kShip6Skm, false, false, 0, kShip6Ulong, kShip6Pair, false, false, 0, 0, 0, kShip6Wt,
-                     kShip6Heavy>
-            <<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+        echo_round_kernel<false, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (opts == 0)  // one round of sub-tiles, writes as soon as a wave has read
-        echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, false, false, false, kShip6Mid, kShip6D2, kShip6Skm,
-                     true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+        echo_round_kernel<false, true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (!small)  // wire mode: 128-B windows, one tile per wave per round
-        echo_kernel6<kShip6U, 1, kShip6Sync, kShip6Stream, false, false, true, false, false, false, false, false, false,
-                     false, 0, kShip6Ulong, false, false, false, 0, 0, 0, kShip6Wt><<<dim3(grid), dim3(kThreads6), 0, s>>>(
-            args, tiles_per_wg);
+        echo_round_kernel<true, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else
-        echo_kernel6<kShip6U, 1, 0, kShip6Stream, false, false, true, false, false, false, false, false, true>
-            <<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+        echo_round_kernel<true, true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     const hipError_t le = hipGetLastError();
     timer_end(slot, s);
     if (le != hipSuccess) return xsk_gpu__hip_fail(le);
@@ -233,6 +230,16 @@ int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size, const str
                                      struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream, uint32_t tile) {
     return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 1,
                        tile);
+}
+
+// Internal (tests / tools, not in include/xsk_gpu.h): xsk_gpu_echo_dev_opts with the workgroup count of a
+// large batch forced to `grid` (0 = one per CU), so that shares of several rounds -- paired short tiles,
+// uniform and ranked streams in every round of a share -- run on small batches too.
+int xsk_gpu__echo_dev_grid(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
+                           void* d_workspace, void* stream, uint32_t grid) {
+    return echo_launch(d_umem, umem_size, d_descs, n, opts, d_verdicts, d_recs, d_stats, d_workspace, stream, 0, 0,
+                       grid);
 }
 
 int xsk_gpu_timing_enable(int enable) {

@@ -6,6 +6,7 @@
 #define XSK_GPU_INTERNAL_H
 
 #include "../../include/xsk_gpu.h"
+#include "xsk_lowlat_proto.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -26,6 +27,12 @@ XSK_GPU__HIDDEN int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem
                                                      uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs,
                                                      struct xsk_gpu_stats* d_stats, void* d_workspace, void* stream,
                                                      uint32_t tile);
+
+/* xsk_echo.hip (exported for tests and tools, not part of the ABI): xsk_gpu_echo_dev_opts with the workgroup
+ * count of a large batch (n > XSK_GPU_LOWLAT_MAX) forced to `grid` (0 = one per CU). */
+int xsk_gpu__echo_dev_grid(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                           uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
+                           void* d_workspace, void* stream, uint32_t grid);
 
 /* Frames per wave for a small batch (n <= XSK_GPU_LOWLAT_MAX) whose frames are read across PCIe: about
  * 8 KiB of frame bytes per wave, 1..16 waves (a 64-frame batch of minimum-size frames is one wave: its
@@ -48,26 +55,8 @@ XSK_GPU__HIDDEN int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* um
                                          uint32_t max_batch, int mode);
 XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
 
-/* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context.  Shared memory
- * layout (mapped, fine-grained pinned host memory): every word the host spins on or the kernel polls sits
- * on a 64-byte line of its own. */
-struct xsk_gpu__bell {
-    /* host -> device: ONE 64-bit word, so a poll is one PCIe read:
-     *   bits 0-31 seq (bumped by one per posted batch), 32-47 n (<= XSK_GPU_LOWLAT_MAX),
-     *   bit 48 write records, bits 49-55 frames per wave / 4 (0: ceil(n / 16)),
-     *   bit 63 stop (the persistent kernel exits at its next poll) */
-    volatile uint64_t cmd;
-    uint32_t pad0[14];
-    /* the same word again in a line of its own: the kernel keeps two polls in flight, one per copy (two
-     * reads of ONE line do not overlap -- the second waits for the first) */
-    volatile uint64_t cmd_b;
-    uint32_t pad0b[14];
-    /* device -> host */
-    volatile uint32_t done;  /* seq of the last completed batch */
-    volatile uint32_t alive; /* 1 while the persistent kernel runs */
-    uint32_t pad2[14];
-};
-
+/* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context (doorbell layout and
+ * host protocol: xsk_lowlat_proto.h). */
 /* Diagnostics of a LOWLAT kernel, in DEVICE memory (a store to host memory would put a PCIe
  * acknowledgement in front of the next doorbell poll), read by xsk_gpu__lowlat_trace().  100-MHz ticks. */
 struct xsk_gpu__lldiag {
@@ -78,12 +67,10 @@ struct xsk_gpu__lldiag {
     uint64_t clk[2];    /* shader-clock (s_memtime) ticks and wall ticks over the last body */
     uint64_t polls[3];  /* this kernel instance: batches served, doorbell reads examined, reads that saw a
                          * new doorbell with descriptor slots not yet tagged */
+    uint32_t exit_gen;  /* the leader's idle exit: the launch generation that is leaving (the other resident
+                         * workgroups poll it and leave too) */
+    uint32_t pad;
 };
-#define XSK_GPU__BELL_N(n) ((uint64_t)(n) << 32)
-#define XSK_GPU__BELL_RECS (1ull << 48)
-#define XSK_GPU__BELL_TILE(q) ((uint64_t)((q) & 0x7Fu) << 49)
-#define XSK_GPU__BELL_STOP (1ull << 63)
-
 typedef struct xsk_gpu__lowlat xsk_gpu__lowlat;
 /* Create the channel on the current device for the (mapped) UMEM alias d_umem: its doorbell, mapped
  * buffers and stream.  The persistent kernel starts with the first batch. */
@@ -93,6 +80,8 @@ XSK_GPU__HIDDEN void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts);
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
+/* 1 while a timed-out batch's instance has not stopped (later doorbell calls return -EBUSY). */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_broken(xsk_gpu__lowlat* ll);
 /* Mapped host buffers the kernel reads / writes: descriptors, verdicts, records. */
 XSK_GPU__HIDDEN struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll);
@@ -102,6 +91,11 @@ XSK_GPU__HIDDEN struct xsk_gpu_rec* xsk_gpu__lowlat_recs(xsk_gpu__lowlat* ll);
  * the shader clock over the last body, in MHz; out[10..11] the host's time from entry to the doorbell
  * store and from there to seeing the completion. */
 int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[15]);
+/* Tuning / test knobs of a LOWLAT context (exported for tools/hostlat.py and the GPU tests; not part of the
+ * ABI): frames per wave of a doorbell batch (multiple of 4 in [4, 64]; 0 = from the batch's bytes), the
+ * workgroups that serve it (1..XSK_GPU__LL_WG; 0 = from its size), and the completion timeout in
+ * microseconds (0 = 2 s).  -EINVAL for a non-LOWLAT context or values out of range. */
+int xsk_gpu__lowlat_tune(xsk_gpu_ctx* ctx, uint32_t tile_frames, uint32_t groups, uint32_t timeout_us);
 XSK_GPU__HIDDEN xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* ctx);
 
 #ifdef __cplusplus

@@ -1,0 +1,206 @@
+/*
+ * xsk_lowlat_proto.h — host side of the LOWLAT doorbell protocol (C11 / C++, no HIP types): the shared
+ * doorbell layout, the command word, the choice of resident workgroups per batch, and the post / wait /
+ * recover state machine of one call.  The HIP plumbing (launch, stream query) comes in through callbacks,
+ * so the state machine -- in particular its timeout and recovery paths -- is unit-tested on the CPU
+ * (tests/c/test_lowlat_proto.c) against a simulated kernel.
+ *
+ * The reference hands its transform RX_BATCH_SIZE = 64 descriptors per poll() (src/lib/xsk_receive.c:196,
+ * :251-257; src/lib/xsk_utils.h:8); xsk_lowlat.hip keeps XSK_GPU__LL_WG workgroups of the round kernel
+ * resident so that such a batch costs a doorbell store and a spin instead of a launch and a stream sync.
+ */
+#ifndef XSK_LOWLAT_PROTO_H
+#define XSK_LOWLAT_PROTO_H
+
+#include <errno.h>
+#include <stdint.h>
+
+#include "../../include/xsk_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* xsk_gpu__ll_slice runs on both sides (the kernel computes its own slice): a host+device function when
+ * compiled by hipcc, a plain C function in the C sources and the CPU unit test. */
+#ifdef __HIPCC__
+#define XSK_GPU__HOSTDEV __host__ __device__
+#else
+#define XSK_GPU__HOSTDEV
+#endif
+
+/* Resident workgroups of a LOWLAT channel (one CU each while it serves).  Workgroup 0 is the leader: it
+ * polls the doorbell AND the first 64 descriptor slots, owns `alive`, and decides the idle exit; the others
+ * poll the command word only and leave when the leader does. */
+#define XSK_GPU__LL_WG 4u
+
+/* Shared doorbell (mapped, fine-grained pinned host memory): every word the host spins on or the kernel
+ * polls sits on a 64-byte line of its own. */
+struct xsk_gpu__bell {
+    /* host -> device: ONE 64-bit word, so a poll is one PCIe read:
+     *   bits 0-31 seq (bumped by one per posted batch), 32-47 n (<= XSK_GPU_LOWLAT_MAX),
+     *   bit 48 write records, bits 49-55 frames per wave / 4 (0: ceil(slice / 16)),
+     *   bits 56-58 workgroups serving the batch (1..XSK_GPU__LL_WG), bit 63 stop (every workgroup exits at
+     *   its next poll) */
+    volatile uint64_t cmd;
+    uint32_t pad0[14];
+    /* the same word again in a line of its own: the leader keeps two polls in flight, one per copy (two
+     * reads of ONE line do not overlap -- the second waits for the first) */
+    volatile uint64_t cmd_b;
+    uint32_t pad0b[14];
+    /* device -> host, one line per workgroup: seq of the last batch it completed (its slice written back);
+     * wg[0].alive = 1 while the leader runs */
+    struct {
+        volatile uint32_t done;
+        volatile uint32_t alive;
+        uint32_t pad[14];
+    } wg[XSK_GPU__LL_WG];
+};
+
+#define XSK_GPU__BELL_N(n) ((uint64_t)(n) << 32)
+#define XSK_GPU__BELL_RECS (1ull << 48)
+#define XSK_GPU__BELL_TILE(q) ((uint64_t)((q) & 0x7Fu) << 49)
+#define XSK_GPU__BELL_WG(w) ((uint64_t)((w) & 0x7u) << 56)
+#define XSK_GPU__BELL_STOP (1ull << 63)
+
+/* Workgroups for a doorbell batch: one per 256 frames or per 256 KiB of frame bytes, 1..XSK_GPU__LL_WG (one
+ * CU caps the PCIe reads of a batch at ~17 GB/s: its waves have only so many loads in flight).  A batch of
+ * <= 64 frames always runs on the leader alone, whose poll already brought its descriptors. */
+static inline uint32_t xsk_gpu__ll_groups(const struct xsk_gpu_desc* d, uint32_t n) {
+    if (n <= 64u) return 1u;
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < n; i++) bytes += d[i].len < 4096u ? d[i].len : 4096u;
+    uint64_t w = (n + 255u) / 256u;
+    const uint64_t wb = (bytes + (256u << 10) - 1u) / (256u << 10);
+    if (wb > w) w = wb;
+    if (w > XSK_GPU__LL_WG) w = XSK_GPU__LL_WG;
+    return (uint32_t)(w < 1 ? 1 : w);
+}
+
+/* Frames of workgroup g's slice of an n-frame batch over w workgroups: contiguous, a multiple of 4 frames
+ * (one 16-lane row per frame and step) except the last. */
+static inline XSK_GPU__HOSTDEV void xsk_gpu__ll_slice(uint32_t n, uint32_t w, uint32_t g, uint32_t* f0, uint32_t* f1) {
+    uint32_t per = (n + w - 1u) / w;
+    per = (per + 3u) & ~3u;
+    const uint32_t a = g * per < n ? g * per : n;
+    *f0 = a;
+    *f1 = a + per < n ? a + per : n;
+}
+
+/* Callbacks into the HIP side (xsk_lowlat.hip) or a simulation (tests/c/test_lowlat_proto.c). */
+struct xsk_gpu__ll_ops {
+    void* u;
+    int (*launch)(void* u);      /* enqueue one instance of the resident grid on its stream: 0 or -errno */
+    int (*stream_idle)(void* u); /* 1: no instance is running or queued on the stream */
+    double (*now)(void* u);      /* seconds, monotonic */
+    void (*relax)(void* u);      /* one spin-wait step */
+};
+
+struct xsk_gpu__ll_state {
+    struct xsk_gpu__bell* bell;
+    uint32_t seq;         /* last posted batch */
+    int launched;         /* an instance was launched and may still run */
+    int broken;           /* a timed-out batch whose instance had not stopped when the call returned */
+    double timeout_s;     /* a batch not complete after this long: -ETIMEDOUT */
+    double quiesce_s;     /* after a timeout, how long to wait for the instance to stop */
+    double recheck_s;     /* while waiting, how often to check that an instance is still there */
+};
+
+static inline void xsk_gpu__ll_post(struct xsk_gpu__bell* b, uint64_t c) {
+    __atomic_store_n(&b->cmd_b, c, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&b->cmd, c, __ATOMIC_SEQ_CST);
+}
+
+/* Stop the resident grid (xsk_gpu_fini, a large batch, new options): post STOP keeping the last seq, and
+ * wait up to `wait_s` (< 0: for ever) for the stream to drain.  Returns 0 once no instance runs, -ETIMEDOUT
+ * if one still did at the deadline (the channel is then `broken`). */
+static inline int xsk_gpu__ll_stop(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, double wait_s) {
+    if (!st->launched && !st->broken) return 0;
+    xsk_gpu__ll_post(st->bell, (uint64_t)st->seq | XSK_GPU__BELL_STOP);
+    const double t0 = ops->now(ops->u);
+    for (;;) {
+        if (ops->stream_idle(ops->u)) {
+            st->launched = 0;
+            st->broken = 0;
+            return 0;
+        }
+        if (wait_s >= 0 && ops->now(ops->u) - t0 > wait_s) {
+            st->broken = 1;
+            return -ETIMEDOUT;
+        }
+        ops->relax(ops->u);
+    }
+}
+
+/* One doorbell batch: the caller has written the descriptors (slots 0 .. n-1, the `options` of the first 64
+ * tagged with seq + 1, the seq this call posts) into the mapped buffer.  `bits` = the n / records / tile fields; w = serving
+ * workgroups.  Returns 0 when every serving workgroup has published completion (the caller's outputs are
+ * then in the mapped buffers), or:
+ *   -EBUSY      an earlier call timed out and its instance has still not stopped: nothing was posted;
+ *   -ETIMEDOUT  the batch did not complete within timeout_s: STOP was posted and the instance waited for
+ *               (quiesce_s); once it has stopped the caller owns its frames again (the batch may or may not
+ *               have been transformed), else the channel stays `broken` and later calls return -EBUSY until
+ *               it has;
+ *   a launch error. */
+static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, uint64_t bits,
+                                  uint32_t w) {
+    struct xsk_gpu__bell* b = st->bell;
+    if (st->broken) {
+        if (!ops->stream_idle(ops->u)) return -EBUSY;
+        st->broken = 0;
+        st->launched = 0;
+    }
+    int fresh = 0; /* an instance launched by this call: it takes its baselines from `done` and serves seq */
+    if (!st->launched || !__atomic_load_n(&b->wg[0].alive, __ATOMIC_SEQ_CST)) {
+        /* gone (idle exit) or never started: launch; stream order puts it behind an exiting instance */
+        const int rc = ops->launch(ops->u);
+        if (rc) return rc;
+        st->launched = 1;
+        fresh = 1;
+    }
+    const uint32_t seq = st->seq + 1u;
+    st->seq = seq;
+    xsk_gpu__ll_post(b, (uint64_t)seq | bits | XSK_GPU__BELL_WG(w));
+    if (!fresh && !__atomic_load_n(&b->wg[0].alive, __ATOMIC_SEQ_CST)) {
+        /* the leader was leaving (Dekker: it re-reads the doorbell after clearing alive, or this launch serves
+         * the batch) */
+        const int rc = ops->launch(ops->u);
+        if (rc) return rc;
+    }
+    const double t_post = ops->now(ops->u);
+    double t_check = t_post;
+    for (uint32_t spin = 0;; ++spin) {
+        uint32_t g = 0;
+        while (g < w && __atomic_load_n(&b->wg[g].done, __ATOMIC_ACQUIRE) == seq) ++g;
+        if (g == w) break;
+        if ((spin & 255u) == 255u) {
+            const double t = ops->now(ops->u);
+            if (t - t_check > st->recheck_s) {
+                t_check = t;
+                /* every instance has exited without serving the batch: serve it now (a relaunched grid takes
+                 * each workgroup's baseline from its `done`, so nothing is served twice) */
+                if (ops->stream_idle(ops->u)) {
+                    uint32_t h = 0;
+                    while (h < w && __atomic_load_n(&b->wg[h].done, __ATOMIC_ACQUIRE) == seq) ++h;
+                    if (h < w) {
+                        const int rc = ops->launch(ops->u);
+                        if (rc) return rc;
+                    }
+                }
+            }
+            if (t - t_post > st->timeout_s) {
+                (void)xsk_gpu__ll_stop(st, ops, st->quiesce_s);
+                return -ETIMEDOUT;
+            }
+        }
+        ops->relax(ops->u);
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return 0;
+}
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* XSK_LOWLAT_PROTO_H */
