@@ -20,7 +20,7 @@ DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip
 BUILD_ID := $(shell cat $(CSRC)/xsk_echo.hip $(DEVHDR) | sha256sum | cut -c1-16)-$(shell echo '$(HIPFLAGS)' | sha256sum | cut -c1-4)
 HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_lowlat.o
 HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o
-TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o
+TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o $(CSRC)/tune/xsk_tune_product.o
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -28,7 +28,7 @@ $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 $(CSRC)/xsk_echo.o: $(CSRC)/xsk_echo.hip $(DEVHDR) Makefile
 	$(HIPCC) $(HIPFLAGS) -DXSK_GPU_BUILD_ID='"$(BUILD_ID)"' -c -o $@ $<
 
-$(CSRC)/tune/%.o: $(CSRC)/tune/%.hip $(DEVHDR) $(CSRC)/tune/xsk_echo_variants.h
+$(CSRC)/tune/%.o: $(CSRC)/tune/%.hip $(DEVHDR) $(CSRC)/tune/xsk_echo_variants.h $(CSRC)/tune/xsk_echo_lab.h
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(CSRC)/%.o: $(CSRC)/%.c include/xsk_gpu.h $(CSRC)/xsk_gpu_internal.h $(CSRC)/xsk_ring.h

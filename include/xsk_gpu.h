@@ -58,7 +58,8 @@ struct xsk_gpu_desc {
  * Accumulated, never reset, by every call:
  *   rx_packets += n                      (xsk_receive.c:233)
  *   rx_bytes   += sum(len)   all frames  (xsk_receive.c:229)
- *   tx_packets += #TX_REPLY              (xsk_receive.c:172; the library assumes sendto succeeds)
+ *   tx_packets += #TX_REPLY              (xsk_receive.c:172; sendto assumed to succeed: see
+ *                                         xsk_gpu_stats_tx_failed() to apply the real outcome)
  *   tx_bytes   += sum(len)   TX_REPLY    (xsk_receive.c:171)
  * `timestamp` is never touched (the reference's stats thread owns it, xsk_stats.c:83). */
 struct xsk_gpu_stats {
@@ -201,9 +202,22 @@ enum xsk_gpu_mode {
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode);
 
 /* Synchronously process one batch of host descriptors against the bound UMEM.  Same outputs as
- * xsk_gpu_echo_dev(); `verdicts`, `recs` and `stats` are host pointers (each may be NULL). */
+ * xsk_gpu_echo_dev(); `verdicts`, `recs` and `stats` are host pointers (each may be NULL).
+ * XSK_GPU_MODE_LOWLAT: if a doorbell batch is not complete within 2 s the call posts STOP, waits (up to 1 s)
+ * for the resident kernel to stop and returns -ETIMEDOUT; the caller then owns that batch's frames again
+ * (each may or may not have been transformed).  If the kernel had not stopped by then, every later call
+ * returns -EBUSY, touching nothing, until it has (xsk_gpu_fini() waits for it). */
 int xsk_gpu_process(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                     struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+
+/* The reference counts a reply in tx_packets / tx_bytes only after its sendto() succeeded
+ * (xsk_receive.c:166-172); every entry point above counts each TX_REPLY frame as sent.  A caller that sends the
+ * replies itself reports the outcome here: for every i with verdicts[i] == XSK_GPU_TX_REPLY and sent[i] == 0,
+ * tx_packets -= 1 and tx_bytes -= descs[i].len, so the counters end where the reference's would.  Host memory
+ * only, no device call.  Returns the number of frames taken back (never more than the counters hold), or
+ * -EINVAL. */
+int xsk_gpu_stats_tx_failed(struct xsk_gpu_stats* stats, const struct xsk_gpu_desc* descs, const uint8_t* verdicts,
+                            const uint8_t* sent, uint32_t n);
 
 /* Wire-format options (XSK_GPU_OPT_*) for this context's later xsk_gpu_process() / xsk_gpu_rx_step()
  * calls (0 at init: the reference's gates). */
@@ -222,16 +236,29 @@ typedef struct xsk_gpu_multi xsk_gpu_multi;
 
 /* Bind G = ndev contexts (devices[g], repeats allowed: G contexts on one GPU) to ONE caller UMEM
  * (registered once with the HIP runtime, portable + mapped, for every device).  `mode` and
- * `max_batch` as for xsk_gpu_init(); max_batch bounds the whole batch of later calls. */
+ * `max_batch` as for xsk_gpu_init(); max_batch bounds the whole batch of later calls.
+ * Device memory: a STAGED context holds a full umem_size mirror of the UMEM on its device (a share's frames
+ * lie anywhere in it), so contexts that repeat a device need G x umem_size there; ZEROCOPY and LOWLAT
+ * contexts read the UMEM in place and hold only per-batch buffers. */
 int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, void* umem, uint64_t umem_size,
                        uint32_t max_batch, int mode);
 
 /* xsk_gpu_process() of one batch over the G contexts: descriptor i goes to context i mod G (frames
  * are independent, xsk_receive.c:113-190), each context runs on its own host thread and stream, and
  * verdicts / records land at the descriptors' own positions.  The four counters are the sum over the
- * contexts (xsk_utils.h:17-23), added to *stats like xsk_gpu_process() does. */
+ * contexts (xsk_utils.h:17-23), added to *stats like xsk_gpu_process() does.
+ * LOWLAT contexts: the path is chosen per batch -- when a share exceeds XSK_GPU_LOWLAT_MAX every context
+ * takes the launch path, so shares of one batch never split between resident kernels and launched grids.
+ * Partial failure: when any context fails, the call returns the first failing context's error and adds
+ * NOTHING to *stats (all or nothing); the shares of the contexts that succeeded are transformed and their
+ * verdicts / records written, the failed shares' positions are left as they were -- xsk_gpu_multi_status()
+ * says which is which. */
 int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                           struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
+
+/* Per-context result of the last xsk_gpu_multi_process(): status[g] = 0 or that context's negative errno for
+ * the share of descriptors i with i mod G == g (at most `cap` entries written).  Returns G. */
+int xsk_gpu_multi_status(const xsk_gpu_multi* m, int* status, uint32_t cap);
 
 /* Wire-format options for every context (xsk_gpu_set_options). */
 int xsk_gpu_multi_set_options(xsk_gpu_multi* m, uint32_t opts);

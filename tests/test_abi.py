@@ -150,8 +150,8 @@ def test_tuning_code_is_not_in_the_product_library():
     # the product exports the C ABI, plus the CU count the tuning library links against and a
     # diagnostics hook of the LOWLAT channel (tools/echo_replay)
     exported = set(re.findall(r"\bT (\w+)", prod))
-    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu", "xsk_gpu__lowlat_trace",
-                                                    "xsk_gpu__echo_dev_grid"}, \
+    assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu", "xsk_gpu__lowlat_trace", "xsk_gpu__lowlat_tune",
+                                                    "xsk_gpu__echo_dev_grid", "xsk_gpu__multi_inject"}, \
         exported - set(declared_functions())
     tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
                           check=True).stdout
@@ -180,3 +180,31 @@ def test_multi_and_lowlat_validation_without_gpu():
     hdr = open(HEADER).read()
     assert "XSK_GPU_MODE_LOWLAT = 2" in hdr and f"XSK_GPU_LOWLAT_MAX {X.LOWLAT_MAX}u" in hdr
     assert f"XSK_GPU_MULTI_MAX {X.MULTI_MAX}" in hdr
+
+
+def test_product_reads_no_environment():
+    """No process-global switch in the product: libxsknet_amd.so imports no getenv / secure_getenv (tuning knobs
+    are explicit entry points of the tools)."""
+    import xsknet_amd as X
+    undef = subprocess.run(["nm", "-D", "--undefined-only", X.LIB_PATH], capture_output=True, text=True,
+                           check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", undef), [l for l in undef.splitlines() if "getenv" in l]
+
+
+def test_multi_fold_all_or_nothing_c_unit():
+    """xsk_gpu_multi_process's counter fold (xsk_gpu__multi_fold, xsk_gpu_internal.h): every share's counters
+    when all succeeded, none and the first error when any failed (an injected failing context)."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        exe = os.path.join(td, "t")
+        subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Werror", "-I", "/opt/rocm/include", "-o", exe,
+                        os.path.join(ROOT, "tests", "c", "test_multi_fold.c")], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    assert "multi fold ok" in out
+
+
+def test_multi_status_validation_without_gpu():
+    import xsknet_amd as X
+    L = X.lib()
+    st = (C.c_int * 4)()
+    assert L.xsk_gpu_multi_status(None, st, 4) == -errno.EINVAL

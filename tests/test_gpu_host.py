@@ -199,11 +199,13 @@ def test_multi_context_argument_checks():
     L.xsk_gpu_multi_fini(None)
 
 
-def test_lowlat_posts_near_idle_exit():
+@pytest.mark.parametrize("batch", [64, 512])
+def test_lowlat_posts_near_idle_exit(batch):
     """Batches posted right around the resident kernel's 50-ms idle exit (the exit / relaunch race): every
-    batch is served exactly once and exactly right."""
+    batch is served exactly once and exactly right -- 64-frame batches (the leader alone) and 512-frame
+    batches served by two resident workgroups (the leader's exit takes the other workgroup with it)."""
     _dev()
-    n, batch = 64 * 40, 64
+    n = batch * 40
     umem = np.zeros(n * 2048, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2323, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
@@ -221,3 +223,131 @@ def test_lowlat_posts_near_idle_exit():
     for k in COUNTERS:
         assert tot[k] == int(s_ref[k]), k
     assert (work == ref).all()
+
+
+@pytest.mark.parametrize("groups", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("flen", [64, 1500])
+def test_lowlat_workgroup_slices(groups, flen):
+    """Doorbell batches of 65-1024 frames served by 1-4 resident workgroups (0: chosen from the batch's size),
+    each a contiguous slice of the descriptors: every verdict, record, counter and byte exact, consecutive
+    batches of different sizes so a workgroup's slice moves between calls, plus one-frame and 64-frame calls
+    (the leader alone) in between."""
+    _dev()
+    sizes = [65, 1024, 256, 1, 300, 777, 64, 1023, 4, 1024]
+    n = sum(sizes)
+    umem = np.zeros(n * 2048 + 4096, np.uint8)
+    mode = 0 if flen == 1500 else 1
+    descs = oracle.synth_batch(umem, n, 256, 2048, seed=0x5EED2424 + groups + flen, mode=mode, len_lo=20 if mode else flen,
+                               len_hi=flen)
+    work = umem.copy()
+    tot = {k: 0 for k in COUNTERS}
+    vs, rs = [], []
+    with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
+        ctx.lowlat_tune(groups=groups)
+        a = 0
+        for m in sizes:
+            v, r, st = ctx.process(descs[a:a + m])
+            vs.append(v)
+            rs.append(r)
+            for k in tot:
+                tot[k] += int(st[k])
+            a += m
+    check(umem, work, descs, np.concatenate(vs), np.concatenate(rs), tot)
+
+
+def test_lowlat_timeout_quiesces_and_recovers():
+    """A doorbell batch that misses its completion timeout (set to 1 us here, so a 1024 x 1500-B batch cannot
+    make it): the call returns -ETIMEDOUT only after STOP has been posted and the resident grid has stopped, so
+    the caller owns its frames again -- each frame of that batch is either untouched or exactly transformed and
+    nothing changes it afterwards; the next call (default timeout) relaunches the grid and is exact."""
+    import errno
+    _dev()
+    n = 2048
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2525, mode=0, len_lo=1500, len_hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, _ = oracle.echo_batch(ref, descs)
+    work = umem.copy()
+    timed_out = 0
+    with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
+        ctx.process(descs[1024:1025])  # the grid is up
+        work[1024 * 2048:1025 * 2048] = umem[1024 * 2048:1025 * 2048]
+        ctx.lowlat_tune(timeout_us=1)
+        try:
+            ctx.process(descs[:1024])
+        except X.XskGpuError as e:
+            assert e.rc == -errno.ETIMEDOUT, e
+            timed_out = 1
+        snap = work[:1024 * 2048].copy()
+        time.sleep(0.2)  # a kernel still running would change frames now
+        assert (work[:1024 * 2048] == snap).all(), "frames changed after the timed-out call returned"
+        for j in range(1024):
+            f = work[j * 2048:(j + 1) * 2048]
+            assert (f == umem[j * 2048:(j + 1) * 2048]).all() or (f == ref[j * 2048:(j + 1) * 2048]).all(), j
+        ctx.lowlat_tune(timeout_us=0)
+        v, r, _ = ctx.process(descs[1024:])
+    assert (v == v_ref[1024:]).all() and (r == r_ref[1024:]).all()
+    assert (work[1024 * 2048:] == ref[1024 * 2048:]).all()
+    print(f"timed out: {timed_out}")
+
+
+def test_multi_context_partial_failure():
+    """One context of three fails (injected): the call returns its error and adds NOTHING to the counters; the
+    other contexts' shares are transformed with their verdicts / records written, the failed share's frames and
+    output positions are untouched; xsk_gpu_multi_status says which share failed; the next call is whole."""
+    import ctypes as C
+    import errno
+    _dev()
+    n = 6000
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2626, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    for mode in (X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT):
+        for batch in (300, n):  # doorbell-sized shares (LOWLAT) and launched ones
+            work = umem.copy()
+            with X.MultiContext(work, [0, 0, 0], max_batch=batch, mode=mode) as m:
+                m.inject_failure(1, -errno.EIO)
+                d = np.ascontiguousarray(descs[:batch])
+                verd = np.full(batch, 0xEE, np.uint8)
+                recs = np.zeros(batch, X.REC_DTYPE)
+                stats = np.zeros(1, X.STATS_DTYPE)
+                stats["rx_packets"] = 7
+                rc = X.lib().xsk_gpu_multi_process(m._ctx, d.ctypes.data, batch, verd.ctypes.data, recs.ctypes.data,
+                                                   stats.ctypes.data)
+                assert rc == -errno.EIO
+                assert m.status() == [0, -errno.EIO, 0]
+                assert int(stats["rx_packets"][0]) == 7 and int(stats["tx_bytes"][0]) == 0  # nothing added
+                ok = np.arange(batch) % 3 != 1
+                assert (verd[ok] == v_ref[:batch][ok]).all() and (recs[ok] == r_ref[:batch][ok]).all()
+                assert (verd[~ok] == 0xEE).all() and (recs[~ok] == np.zeros(1, X.REC_DTYPE)).all()
+                for j in range(batch):
+                    exp = ref if ok[j] else umem
+                    assert (work[j * 2048:(j + 1) * 2048] == exp[j * 2048:(j + 1) * 2048]).all(), (mode, batch, j)
+                # the next call: every context, counters applied
+                work[:] = umem
+                v, r, st = m.process(descs[:batch])
+                assert m.status() == [0, 0, 0]
+                assert (v == v_ref[:batch]).all() and (r == r_ref[:batch]).all()
+                assert int(st["tx_packets"]) == int((v_ref[:batch] == 0).sum())
+    del C
+
+
+def test_multi_lowlat_path_chosen_per_batch():
+    """LOWLAT contexts sharing one GPU: a batch whose shares straddle the doorbell limit (2049 frames over two
+    contexts: 1025 + 1024) takes the launch path in every context; doorbell-sized batches before and after
+    it go through the resident kernels -- every byte exact."""
+    _dev()
+    n = 2049 + 128 + 2049
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2727, mode=1, len_lo=20, len_hi=1500)
+    work = umem.copy()
+    tot = {k: 0 for k in COUNTERS}
+    vs = []
+    with X.MultiContext(work, [0, 0], max_batch=2049, mode=X.MODE_LOWLAT) as m:
+        for a, b in ((0, 2049), (2049, 2177), (2177, n)):
+            v, _, st = m.process(descs[a:b], want_recs=False)
+            vs.append(v)
+            for k in tot:
+                tot[k] += int(st[k])
+    check(umem, work, descs, np.concatenate(vs), None, tot)

@@ -1,0 +1,135 @@
+"""The LOWLAT kernel's completion ordering, checked in the BUILT code object (no GPU).
+
+A round-end GPU run of round 2 caught `done` overtaking the verdicts about once in 10^4 one-frame calls: ROCm
+7.2 drops the release fence's own `s_waitcnt vmcnt(0)` after `buffer_wbl2` when the wave's scoreboard is
+provably empty, so the completion store could leave before the L2 write-back of the outputs had finished.
+xsk_lowlat.hip places the waits by hand.  This test extracts the gfx950 code object of `lowlat_kernel` from
+libxsknet_amd.so (the .hip_fatbin section's clang offload bundles), disassembles it with llvm-objdump and
+asserts, for both template instances, the sequence
+
+    s_waitcnt vmcnt(0)          every wave: its own stores have been acknowledged
+    s_barrier                   the workgroup meets (no vector-memory op in between)
+    buffer_wbl2 sc0 sc1         thread 0: system-scope release (L2 write-back)
+    s_waitcnt vmcnt(0)          the write-back has completed
+    global_store_dword ... sc0 sc1   bell->wg[g].done = seq
+
+so that a toolchain change that reorders or drops a wait fails here instead of on a GPU once in 10^4 calls.
+"""
+import os
+import re
+import struct
+import subprocess
+import tempfile
+
+import pytest
+
+from tests.conftest import ROOT
+
+LIB = os.path.join(ROOT, "xsknet_amd", "libxsknet_amd.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+VMEM = re.compile(r"^\s*(global|buffer|flat)_(load|store|atomic)")  # scratch reloads of spilled pointers are private
+
+
+def _section(path, name):
+    out = subprocess.run([f"{LLVM}/llvm-readelf", "-S", "-W", path], capture_output=True, text=True,
+                         check=True).stdout
+    for line in out.splitlines():
+        f = line.split()
+        if name in f:
+            i = f.index(name)
+            off, size = int(f[i + 3], 16), int(f[i + 4], 16)
+            with open(path, "rb") as fh:
+                fh.seek(off)
+                return fh.read(size)
+    raise AssertionError(f"{name} not in {path}")
+
+
+def gfx950_code_objects(path):
+    """The gfx950 entries of every clang offload bundle in the library's .hip_fatbin section."""
+    sec = _section(path, ".hip_fatbin")
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    objs, i = [], 0
+    while (j := sec.find(magic, i)) >= 0:
+        n = struct.unpack_from("<Q", sec, j + len(magic))[0]
+        p = j + len(magic) + 8
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", sec, p)
+            p += 24
+            triple = sec[p:p + tl].decode()
+            p += tl
+            if "gfx950" in triple and size:
+                objs.append(sec[j + off:j + off + size])
+        i = j + 1
+    assert objs, "no gfx950 code object in the fat binary (compressed bundles are not expected here)"
+    return objs
+
+
+def done_offset():
+    """offsetof(struct xsk_gpu__bell, wg[0].done) from the protocol header itself (a compiled C probe)."""
+    probe = '#include <stdio.h>\n#include <stddef.h>\n#include "xsk_lowlat_proto.h"\n' \
+            'int main(void){printf("%zu\\n", offsetof(struct xsk_gpu__bell, wg[0].done));return 0;}\n'
+    with tempfile.TemporaryDirectory() as td:
+        c = os.path.join(td, "p.c")
+        open(c, "w").write(probe)
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "xsknet_amd", "csrc"), "-o", os.path.join(td, "p"),
+                        c], check=True)
+        return int(subprocess.run([os.path.join(td, "p")], capture_output=True, text=True, check=True).stdout)
+
+
+def lowlat_functions():
+    """{symbol: [instruction lines]} of every lowlat_kernel instance."""
+    funcs = {}
+    with tempfile.TemporaryDirectory() as td:
+        for k, co in enumerate(gfx950_code_objects(LIB)):
+            p = os.path.join(td, f"co{k}.o")
+            open(p, "wb").write(co)
+            dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", p], capture_output=True, text=True,
+                                 check=True).stdout
+            cur = None
+            for line in dis.splitlines():
+                m = re.match(r"^[0-9a-f]{16} <(\S+)>:", line)
+                if m:
+                    cur = m.group(1) if "lowlat_kernel" in m.group(1) else None
+                    if cur:
+                        funcs[cur] = []
+                elif cur and line.startswith("\t"):
+                    funcs[cur].append(line.split("//")[0].strip())
+    return funcs
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM}/llvm-objdump"), reason="llvm-objdump not installed")
+def test_lowlat_completion_waits_for_the_write_back():
+    funcs = lowlat_functions()
+    off = done_offset()
+    assert len(funcs) == 2, sorted(funcs)  # the reference-mode and the wire-mode instance
+    for name, ins in funcs.items():
+        # the completion store: a system-scope (sc0 sc1) dword store to bell->wg[g].done (the immediate offset of
+        # wg[0].done in the doorbell, the workgroup's line added into the address)
+        done = [i for i, s in enumerate(ins) if re.match(rf"global_store_dword \S+, \S+, .*offset:{off} sc0 sc1$", s)]
+        assert len(done) == 1, (name, [ins[i] for i in done])
+        d = done[0]
+        # walking back from it: a vmcnt(0) wait, and before that the release write-back, with no other
+        # vector-memory op in between
+        j = d - 1
+        saw_wait = False
+        while not ins[j].startswith("buffer_wbl2"):
+            assert not VMEM.match(ins[j]), (name, "a vector-memory op between the write-back and done", ins[j])
+            saw_wait |= ins[j] == "s_waitcnt vmcnt(0)"
+            j -= 1
+            assert j > d - 64, (name, "no buffer_wbl2 before the done store")
+        assert ins[j] == "buffer_wbl2 sc0 sc1", (name, ins[j])
+        assert saw_wait, (name, "no s_waitcnt vmcnt(0) between buffer_wbl2 and the done store")
+        # before the write-back: the workgroup barrier, reached by every wave only after its own stores have
+        # been acknowledged (vmcnt(0) after the wave's last vector-memory op)
+        k = j - 1
+        while ins[k] != "s_barrier":
+            assert not VMEM.match(ins[k]), (name, "a vector-memory op between the barrier and the write-back", ins[k])
+            k -= 1
+            assert k > j - 64, (name, "no s_barrier before the write-back")
+        m = k - 1
+        saw_wait = False
+        while not VMEM.match(ins[m]):
+            saw_wait |= bool(re.match(r"s_waitcnt vmcnt\(0\)", ins[m]))
+            m -= 1
+            assert m > k - 256, (name, "no vector-memory op before the barrier")
+        assert saw_wait, (name, "the wave's last vector-memory op is not waited for before the barrier", ins[m])

@@ -62,3 +62,36 @@ def test_rx_step_empty_ring_and_bad_args():
     assert res.received == 0 and fctr[0] == 0 and tctr[0] == 0 and pool.n_free == 4
     assert L.xsk_gpu_rx_step(None, C.byref(rx), C.byref(fq), C.byref(tx), C.byref(pool), 64, None,
                              None) == -errno.EINVAL
+
+
+def test_stats_tx_failed_applies_sendto_outcomes():
+    """xsk_gpu_stats_tx_failed: the reference counts tx_* only after a successful sendto (xsk_receive.c:166-172);
+    replies whose send failed are taken back out of the counters, nothing else changes."""
+    import errno
+    import oracle
+    import xsknet_amd as X
+    L = X.lib()
+    n = 500
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=77, mode=1, len_lo=20, len_hi=1500)
+    v, _, s = oracle.echo_batch(umem, descs)
+    stats = np.zeros(1, X.STATS_DTYPE)
+    for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes"):
+        stats[k] = s[k]
+    sent = (np.arange(n) % 5 != 0).astype(np.uint8)  # every fifth send fails
+    got = L.xsk_gpu_stats_tx_failed(stats.ctypes.data, descs.ctypes.data, v.ctypes.data, sent.ctypes.data, n)
+    fail = (v == X.TX_REPLY) & (sent == 0)
+    assert got == int(fail.sum())
+    ok = (v == X.TX_REPLY) & (sent == 1)
+    assert int(stats["tx_packets"][0]) == int(ok.sum())
+    assert int(stats["tx_bytes"][0]) == int(descs["len"][ok].sum())
+    assert int(stats["rx_packets"][0]) == int(s["rx_packets"]) and int(stats["rx_bytes"][0]) == int(s["rx_bytes"])
+    # argument checks; frames the counters never counted are refused, the counters untouched
+    assert L.xsk_gpu_stats_tx_failed(None, descs.ctypes.data, v.ctypes.data, sent.ctypes.data, n) == -errno.EINVAL
+    assert L.xsk_gpu_stats_tx_failed(stats.ctypes.data, None, v.ctypes.data, sent.ctypes.data, n) == -errno.EINVAL
+    before = stats.copy()
+    none_sent = np.zeros(n, np.uint8)
+    assert L.xsk_gpu_stats_tx_failed(stats.ctypes.data, descs.ctypes.data, v.ctypes.data, none_sent.ctypes.data,
+                                     n) == -errno.EINVAL
+    assert (stats == before).all()
+    assert L.xsk_gpu_stats_tx_failed(stats.ctypes.data, None, None, None, 0) == 0

@@ -5,7 +5,8 @@ separate `bench.py --variant` runs.  This tool times several variants inside ONE
 never-touched batches: in round r, batch b runs variant V[(b + r) % len(V)], so every variant sees every
 pool position; each launch is bracketed by its own pair of HIP events on the launch stream.  Between rounds
 the pool is regenerated (untimed), so diagnostic variants with wrong results cannot poison the next round.
-Variant -1 is the shipped entry point (xsk_gpu_echo_dev).
+Variant -1 is the shipped entry point (xsk_gpu_echo_dev); 1000 + v is the product kernel's source at the
+alternative switch v of tune/xsk_tune_product.hip (xsk_gpu__product_variant).
 
     python tools/abbench.py --config c3 --variants=-1,131,139 --rounds 3
 """
@@ -55,6 +56,10 @@ def main():
         u = slab[b * bb:(b + 1) * bb]
         if v < 0:
             X.echo_dev(u, descs[b], n, verd, recs, stats, ws, stream)
+        elif v >= 1000:
+            rc = tune.xsk_gpu__product_variant(v - 1000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
+                                               verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
+            assert rc == 0, rc
         else:
             rc = tune.xsk_gpu__echo_variant(v, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n, verd.data_ptr(),
                                             recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)

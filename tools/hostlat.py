@@ -29,14 +29,17 @@ def run_one(exe, p, flen, mode, batch, tile, args):
         (["huge=1"] if args.huge else [])
     if args.gpus:
         cmd.insert(7, f"gpus={args.gpus}")
-    env = dict(os.environ, XSK_GPU_LOWLAT_TILE=tile) if tile else None
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    if tile:
+        cmd.append(f"tile={tile}")
+    if args.groups:
+        cmd.append(f"groups={args.groups}")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "error": r.stderr[-300:]}))
         sys.exit(1)
     kv = dict(x.split("=") for x in r.stdout.split())
     us = float(kv["us_per_call"])
-    rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto",
+    rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto", "groups": args.groups or "auto",
            "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge),
            "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3), "calls": int(kv["calls"])}
     if "trace_ns" in kv:  # LOWLAT: the last batch's phases on the GPU
@@ -61,7 +64,8 @@ def main():
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--flush", action="store_true", help="evict the UMEM from the CPU caches before each pass")
     ap.add_argument("--huge", action="store_true", help="the UMEM on transparent huge pages (2 MiB)")
-    ap.add_argument("--tiles", default="", help="LOWLAT frames per wave to sweep (XSK_GPU_LOWLAT_TILE), e.g. 4,16,64")
+    ap.add_argument("--tiles", default="", help="LOWLAT frames per wave to sweep (echo_replay tile=), e.g. 4,16,64")
+    ap.add_argument("--groups", type=int, default=0, help="LOWLAT serving workgroups (echo_replay groups=; 0: by size)")
     args = ap.parse_args()
     exe = os.path.join(ROOT, "tools", "echo_replay")
     n, chunk = 4096, 4096

@@ -114,6 +114,10 @@ _SIGS = {
     "xsk_gpu_multi_init": ([C.POINTER(_P), _P, C.c_uint32, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
     "xsk_gpu_multi_process": ([_P, _P, C.c_uint32, _P, _P, _P], C.c_int),
     "xsk_gpu_multi_set_options": ([_P, C.c_uint32], C.c_int),
+    "xsk_gpu_multi_status": ([_P, _P, C.c_uint32], C.c_int),
+    "xsk_gpu_stats_tx_failed": ([_P, _P, _P, _P, C.c_uint32], C.c_int),
+    "xsk_gpu__multi_inject": ([_P, C.c_uint32, C.c_int], C.c_int),
+    "xsk_gpu__lowlat_tune": ([_P, C.c_uint32, C.c_uint32, C.c_uint32], C.c_int),
     "xsk_gpu_multi_fini": ([_P], None),
     # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
     "xsk_gpu__echo_dev_grid": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32], C.c_int),
@@ -121,6 +125,7 @@ _SIGS = {
 _TUNE_SIGS = {
     "xsk_gpu__echo_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
     "xsk_gpu__echo_wire_variant": ([C.c_int, _P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu__product_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
 }
 _tune: Optional[C.CDLL] = None
 
@@ -273,6 +278,11 @@ class EchoContext:
             stats.ctypes.data))
         return verdicts, recs, stats[0]
 
+    def lowlat_tune(self, tile_frames: int = 0, groups: int = 0, timeout_us: int = 0) -> None:
+        """Tool / test knobs of a LOWLAT context (xsk_gpu__lowlat_tune): frames per wave, serving workgroups,
+        completion timeout (0 = defaults)."""
+        _check("xsk_gpu__lowlat_tune", lib().xsk_gpu__lowlat_tune(self._ctx, tile_frames, groups, timeout_us))
+
     def rx_step(self, rx: Ring, fill: Ring, tx: Ring, pool: FramePool, max_batch: int, stats=None):
         """xsk_gpu_rx_step on this context; returns (received, RxResult)."""
         res = RxResult()
@@ -324,6 +334,18 @@ class MultiContext:
             self._ctx, descs.ctypes.data, n, verdicts.ctypes.data, recs.ctypes.data if recs is not None else None,
             stats.ctypes.data))
         return verdicts, recs, stats[0]
+
+    def status(self):
+        """xsk_gpu_multi_status: per-context result of the last process() (0 or -errno)."""
+        st = (C.c_int * MULTI_MAX)()
+        g = lib().xsk_gpu_multi_status(self._ctx, st, MULTI_MAX)
+        if g < 0:
+            raise XskGpuError("xsk_gpu_multi_status", g)
+        return list(st[:g])
+
+    def inject_failure(self, g: int, rc: int) -> None:
+        """Test hook: context g's next share fails with rc (xsk_gpu__multi_inject)."""
+        _check("xsk_gpu__multi_inject", lib().xsk_gpu__multi_inject(self._ctx, g, rc))
 
     def close(self) -> None:
         if self._ctx:

@@ -277,11 +277,21 @@ out:
 
 int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                     struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats) {
+    return xsk_gpu__process_ex(c, descs, n, verdicts, recs, stats, 0);
+}
+
+int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
+                        struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats, int no_doorbell) {
     int rc = 0;
     if (!c || (!descs && n)) return -EINVAL;
     if (n == 0) return 0;
     if (n > c->max_batch) return -EINVAL;
-    if (c->ll && n <= XSK_GPU_LOWLAT_MAX) { /* the doorbell: no launch, no synchronisation, no HIP call */
+    if (c->ll && xsk_gpu__lowlat_broken(c->ll)) {
+        /* a timed-out doorbell batch whose kernel has not stopped yet may still write: nothing else runs
+         * until it has (-EBUSY), then the context is usable again */
+        if (!xsk_gpu__lowlat_recover(c->ll)) return -EBUSY;
+    }
+    if (c->ll && n <= XSK_GPU_LOWLAT_MAX && !no_doorbell) { /* the doorbell: no launch, no sync, no HIP call */
         memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
         rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL);
         if (rc) return rc;

@@ -48,6 +48,36 @@ static inline uint32_t xsk_gpu__small_tile(const struct xsk_gpu_desc* descs, uin
     return t < 4u ? 4u : (t > 64u ? 64u : t);
 }
 
+/* xsk_gpu_multi.c: fold the G shares of one xsk_gpu_multi_process call into the caller's counters, all or
+ * nothing: when every share succeeded (rc[g] == 0) their counters are added to *out and 0 is returned; when any
+ * failed, *out is left untouched and the first failing share's error is returned (xsk_gpu_multi_status() then
+ * tells which shares were transformed).  Pure host code, unit-tested on the CPU (tests/c/test_multi_fold.c). */
+static inline int xsk_gpu__multi_fold(const int* rc, const struct xsk_gpu_stats* st, uint32_t G,
+                                      struct xsk_gpu_stats* out) {
+    for (uint32_t g = 0; g < G; g++)
+        if (rc[g]) return rc[g];
+    if (out) {
+        for (uint32_t g = 0; g < G; g++) {
+            out->rx_packets += st[g].rx_packets;
+            out->rx_bytes += st[g].rx_bytes;
+            out->tx_packets += st[g].tx_packets;
+            out->tx_bytes += st[g].tx_bytes;
+        }
+    }
+    return 0;
+}
+
+/* xsk_gpu_host.c: xsk_gpu_process with the doorbell path of a LOWLAT context disabled for this call
+ * (no_doorbell != 0: the batch takes the launch path even when it is small) -- the multi-context path decides
+ * per batch, so that shares of one batch never split between the resident kernel and launched grids. */
+XSK_GPU__HIDDEN int xsk_gpu__process_ex(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t n,
+                                        uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats,
+                                        int no_doorbell);
+
+/* xsk_gpu_multi.c (exported for the GPU tests, not part of the ABI): context g's next share fails with `rc`
+ * without being processed (fault injection for the partial-failure semantics). */
+int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
+
 /* xsk_gpu_host.c: xsk_gpu_init over a UMEM the caller has already registered with the HIP runtime
  * (portable + mapped, e.g. the one registration of a multi-GPU object): the context neither registers
  * nor unregisters it. */
@@ -80,8 +110,11 @@ XSK_GPU__HIDDEN void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts);
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
-/* 1 while a timed-out batch's instance has not stopped (later doorbell calls return -EBUSY). */
+/* 1 while a timed-out batch's instance has not stopped (later calls return -EBUSY). */
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_broken(xsk_gpu__lowlat* ll);
+/* A broken channel whose instance has stopped by now becomes usable again: returns 1 if the channel is usable
+ * (never broken, or recovered), 0 while the instance still runs.  Never blocks. */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll);
 /* Mapped host buffers the kernel reads / writes: descriptors, verdicts, records. */
 XSK_GPU__HIDDEN struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN uint8_t* xsk_gpu__lowlat_verdicts(xsk_gpu__lowlat* ll);

@@ -32,6 +32,7 @@ struct multi_worker {
     uint32_t cap;
     struct xsk_gpu_stats st;
     int rc;
+    int inject; /* fault injection (xsk_gpu__multi_inject): the next share fails with this error */
 };
 
 struct xsk_gpu_multi {
@@ -52,6 +53,8 @@ struct xsk_gpu_multi {
     uint32_t job_n;
     uint8_t* job_verd;
     struct xsk_gpu_rec* job_recs;
+    int job_launch; /* every share takes the launch path (a share above XSK_GPU_LOWLAT_MAX) */
+    int status[XSK_GPU_MULTI_MAX]; /* per-context result of the last xsk_gpu_multi_process */
 };
 
 /* Context g's share of the batch: descriptors g, g + G, g + 2G, ... */
@@ -62,8 +65,13 @@ static void run_share(struct multi_worker* w) {
     memset(&w->st, 0, sizeof w->st);
     w->rc = 0;
     if (!k) return;
+    if (w->inject) {
+        w->rc = w->inject;
+        w->inject = 0;
+        return;
+    }
     for (uint32_t j = 0; j < k; j++) w->descs[j] = m->job_descs[g + (size_t)j * G];
-    w->rc = xsk_gpu_process(w->ctx, w->descs, k, w->verd, m->job_recs ? w->recs : NULL, &w->st);
+    w->rc = xsk_gpu__process_ex(w->ctx, w->descs, k, w->verd, m->job_recs ? w->recs : NULL, &w->st, m->job_launch);
     if (w->rc) return;
     if (m->job_verd)
         for (uint32_t j = 0; j < k; j++) m->job_verd[g + (size_t)j * G] = w->verd[j];
@@ -190,6 +198,9 @@ int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, ui
     m->job_n = n;
     m->job_verd = verdicts;
     m->job_recs = recs;
+    /* the path is chosen per batch, not per share: when any share is too large for a LOWLAT doorbell, every
+     * context takes the launch path, so no share runs on a CU that a resident kernel holds */
+    m->job_launch = (n + m->G - 1) / m->G > XSK_GPU_LOWLAT_MAX;
     if (m->G > 1) {
         pthread_mutex_lock(&m->mu);
         m->pending = m->G - 1;
@@ -203,16 +214,22 @@ int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, ui
         while (m->pending) pthread_cond_wait(&m->done, &m->mu);
         pthread_mutex_unlock(&m->mu);
     }
-    int rc = 0;
+    struct xsk_gpu_stats st[XSK_GPU_MULTI_MAX];
     for (uint32_t g = 0; g < m->G; g++) {
-        const struct multi_worker* w = &m->w[g];
-        if (w->rc && !rc) rc = w->rc;
-        if (stats) {
-            stats->rx_packets += w->st.rx_packets;
-            stats->rx_bytes += w->st.rx_bytes;
-            stats->tx_packets += w->st.tx_packets;
-            stats->tx_bytes += w->st.tx_bytes;
-        }
+        m->status[g] = m->w[g].rc;
+        st[g] = m->w[g].st;
     }
-    return rc;
+    return xsk_gpu__multi_fold(m->status, st, m->G, stats);
+}
+
+int xsk_gpu_multi_status(const xsk_gpu_multi* m, int* status, uint32_t cap) {
+    if (!m || (!status && cap)) return -EINVAL;
+    for (uint32_t g = 0; g < m->G && g < cap; g++) status[g] = m->status[g];
+    return (int)m->G;
+}
+
+int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc) {
+    if (!m || g >= m->G || rc >= 0) return -EINVAL;
+    m->w[g].inject = rc;
+    return 0;
 }

@@ -97,3 +97,19 @@ uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_poo
     if (n) xr_cons_release(comp, n); /* :97 */
     return n;
 }
+
+int xsk_gpu_stats_tx_failed(struct xsk_gpu_stats* stats, const struct xsk_gpu_desc* descs, const uint8_t* verdicts,
+                            const uint8_t* sent, uint32_t n) {
+    if (!stats || (n && (!descs || !verdicts || !sent))) return -EINVAL;
+    uint64_t p = 0, b = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (verdicts[i] == XSK_GPU_TX_REPLY && !sent[i]) { /* xsk_receive.c:166-170: no count on a failed send */
+            p++;
+            b += descs[i].len;
+        }
+    }
+    if (p > stats->tx_packets || b > stats->tx_bytes) return -EINVAL; /* not frames these counters counted */
+    stats->tx_packets -= p;
+    stats->tx_bytes -= b;
+    return (int)(p > 0x7FFFFFFFu ? 0x7FFFFFFF : p);
+}

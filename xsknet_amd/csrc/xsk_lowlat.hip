@@ -67,6 +67,129 @@ __device__ __forceinline__ void st_sys(volatile uint32_t* p, uint32_t v) {
     __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Wave 0's doorbell poll until a batch for this workgroup (or the exit).  LEADER is a template parameter, not a
+// runtime test: the two polls in flight are waited for by counting (s_waitcnt vmcnt(N)), and a load issued under
+// a runtime condition makes the compiler wait for every outstanding load instead -- the doorbell was then
+// sampled once per round trip (~1.1 us) instead of every half round trip.
+struct PollState {
+    uint32_t served;
+    uint64_t cA, aA, bA, cB, aB, bB;  // the two polls' registers: they stay live across the body
+    uint64_t t_seen, t_poll, n_batches, n_polls, n_stale;
+};
+template <bool LEADER>
+__device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc, uint32_t* s_cmd, PollState& P,
+                                              uint32_t g, uint32_t lane) {
+    xsk_gpu__bell* bell = L.bell;
+    // wave 0 polls: the leader's every read brings the command word AND the first 64 descriptor slots,
+    // so a batch of <= 64 frames needs no second round trip for its descriptors; the host tags each
+    // slot's `options` with the batch's sequence number, and a slot seen with an older tag (its write
+    // not yet visible) makes the wave poll again.  The other workgroups read the command word only.
+    uint32_t work = 0, n = 0, recs = 0, tq = 0, dl = 0, f0 = 0;
+    uint64_t t0 = wall_clock64(), tr = 0, it = 0;
+    const uint64_t t_loop = t0;
+    // Two polls in flight, issued half a PCIe round trip apart (relaxed system-scope loads: no
+    // wait at issue; the acquire fence follows the barrier below), so the doorbell is sampled
+    // every ~0.6 us instead of every round trip.
+    // A descriptor slot is read with ONE 16-byte load (system-coherent: sc0 sc1), so the tag in its
+    // `options` word and its addr / len come from one snapshot of the host's cache line: a slot seen
+    // with the new tag has the new descriptor (the host writes the descriptor, then the tag, then
+    // the doorbell; x86 keeps that order).  Two separate 8-byte reads could tear.
+    // The two polls read different lines (`cmd` / `cmd_b`, slots 0-63 / their copy after the last
+    // slot): a read of a line that is already being read waits for the first to return, so polls
+    // of one line would sample the doorbell only once per round trip.
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)L.descs, (short)0, (int)((XSK_GPU_LOWLAT_MAX + kTile) * sizeof(xsk_gpu_desc)), kRsrcFlags);
+    constexpr int kSysCoherent = 1 | 16;  // cache policy SC0 | SC1
+    static_assert(kPollCopies == 2, "the loop below alternates two copies");
+    // the other workgroups read a line of their own, one poll at a time (their second "copy" is the
+    // same word: the second read waits for the first)
+    volatile uint64_t* const own = LEADER ? nullptr : &bell->wcmd[g - 1].cmd;
+    auto issue = [&](int copy, uint64_t& c, uint64_t& d0, uint64_t& d1) {
+        c = __hip_atomic_load((uint64_t*)(!LEADER ? own : copy ? &bell->cmd_b : &bell->cmd), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_SYSTEM);
+        if (LEADER) {
+            const int dofs = (int)((copy ? XSK_GPU_LOWLAT_MAX : 0u) * sizeof(xsk_gpu_desc) + lane * 16u);
+            const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(drs, dofs, 0, kSysCoherent);
+            d0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
+            d1 = (uint64_t)d.z | ((uint64_t)d.w << 32);
+        }
+    };
+    // 0: keep polling, 1: a batch for this workgroup, 2: leave
+    auto examine = [&](uint64_t cv, uint64_t d0, uint64_t d1) -> int {
+        ++it;
+        const uint64_t c = ((uint64_t)uniform((uint32_t)(cv >> 32)) << 32) | uniform((uint32_t)cv);
+        tr = (wall_clock64() - t_loop) / it;  // mean sampling interval so far
+        if ((uint32_t)c != P.served) {
+            const uint32_t nn = (uint32_t)(c >> 32) & 0xFFFFu;
+            uint32_t w = (uint32_t)(c >> 56) & 7u;
+            w = w < 1u ? 1u : (w > XSK_GPU__LL_WG ? XSK_GPU__LL_WG : w);
+            if (g >= w) {  // not serving this batch
+                P.served = (uint32_t)c;
+                return 0;
+            }
+            if (LEADER && w == 1u && nn <= (uint32_t)kTile) {
+                if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) {
+                    ++P.n_stale;
+                    return 0;  // not yet
+                }
+                sdesc[lane] = u32x4{(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)};
+                dl = 1;
+            }
+            uint32_t f1 = 0;
+            xsk_gpu__ll_slice(nn > XSK_GPU_LOWLAT_MAX ? XSK_GPU_LOWLAT_MAX : nn, w, g, &f0, &f1);
+            n = f1 - f0;
+            recs = (uint32_t)(c >> 48) & 1u;
+            tq = (uint32_t)(c >> 49) & 0x7Fu;
+            P.served = (uint32_t)c;
+            work = 1;
+            return 1;
+        }
+        if (c & XSK_GPU__BELL_STOP) return 2;
+        if (!LEADER) {  // the leader's idle exit takes every workgroup of this launch with it
+            if (__hip_atomic_load(&L.diag->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L.gen)
+                return 2;
+        } else if (wall_clock64() - t0 > kIdleTicks) {
+            // leaving: clear `alive`, then look once more (the host posts, then reads `alive`)
+            __hip_atomic_store((uint32_t*)&bell->wg[0].alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
+            if (uniform((uint32_t)c2) == P.served || (uniform((uint32_t)(c2 >> 32)) & 0x80000000u)) {
+                __hip_atomic_store(&L.diag->exit_gen, L.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return 2;
+            }
+            st_sys(&bell->wg[0].alive, 1u);
+            t0 = wall_clock64();
+        }
+        return 0;
+    };
+    issue(0, P.cA, P.aA, P.bA);
+    __builtin_amdgcn_s_sleep(22);  // ~0.6 us: half a round trip
+    while (true) {
+        issue(1, P.cB, P.aB, P.bB);
+        int r = examine(P.cA, P.aA, P.bA);  // waits for A only (B is still in flight)
+        if (r) break;
+        issue(0, P.cA, P.aA, P.bA);
+        r = examine(P.cB, P.aB, P.bB);
+        if (r) break;
+    }
+    // ONE system-scope acquire for the workgroup: fresh descriptors and frames.  The doorbell read it
+    // follows has returned (it was examined).  The invalidation completes asynchronously and only
+    // this wave's own later loads are ordered behind it, so the wave waits for it (and for the other
+    // poll, still in flight: at most half a round trip) before the barrier below releases the
+    // other waves' loads (MI355X_MICROARCH.md, cross-CU hand-off recipe).
+    if (work) asm volatile("buffer_inv sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        s_cmd[0] = work;
+        s_cmd[1] = n;
+        s_cmd[2] = recs | (tq << 8) | (dl << 16);
+        s_cmd[3] = f0;
+    }
+    P.t_seen = wall_clock64();
+    P.t_poll = tr;
+    P.n_polls += it;
+    ++P.n_batches;
+}
+
 // XSK_GPU__LL_WG workgroups, one per CU.  Workgroup g serves slice g of a batch posted for w > g workgroups
 // (xsk_gpu__ll_slice) and publishes bell->wg[g].done; workgroup 0 (the leader) also polls the first 64
 // descriptor slots with the doorbell and owns `alive` and the idle exit.
@@ -81,125 +204,17 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
     xsk_gpu__bell* bell = L.bell;
     const uint32_t g = blockIdx.x;
     const bool leader = g == 0;
-    uint32_t served = 0;
-    uint64_t t_seen = 0, t_poll = 0;  // wave 0: diagnostics
-    uint64_t n_batches = 0, n_polls = 0, n_stale = 0;
+    PollState P = {};  // wave 0: `served`, the two polls' registers, diagnostics
     if (threadIdx.x < 64) {  // wave 0 polls; every lane keeps the same `served`
         // this workgroup's last completed batch (a previous instance's; stream order: it has exited)
-        served = uniform(ld_sys(&bell->wg[g].done));
+        P.served = uniform(ld_sys(&bell->wg[g].done));
         if (leader) st_sys(&bell->wg[0].alive, 1u);
     }
     const uint32_t lane = threadIdx.x & 63u;
-    // the two polls' registers live across the body: a batch is taken while the other poll is still in
-    // flight, and registers the compiler reused would first have to wait for it to land
-    uint64_t cA = 0, aA = 0, bA = 0, cB = 0, aB = 0, bB = 0;
     while (true) {
         if (threadIdx.x < 64) {
-            // wave 0 polls: the leader's every read brings the command word AND the first 64 descriptor slots,
-            // so a batch of <= 64 frames needs no second round trip for its descriptors; the host tags each
-            // slot's `options` with the batch's sequence number, and a slot seen with an older tag (its write
-            // not yet visible) makes the wave poll again.  The other workgroups read the command word only.
-            uint32_t work = 0, n = 0, recs = 0, tq = 0, dl = 0, f0 = 0;
-            uint64_t t0 = wall_clock64(), tr = 0, it = 0;
-            const uint64_t t_loop = t0;
-            // Two polls in flight, issued half a PCIe round trip apart (relaxed system-scope loads: no
-            // wait at issue; the acquire fence follows the barrier below), so the doorbell is sampled
-            // every ~0.6 us instead of every round trip.
-            // A descriptor slot is read with ONE 16-byte load (system-coherent: sc0 sc1), so the tag in its
-            // `options` word and its addr / len come from one snapshot of the host's cache line: a slot seen
-            // with the new tag has the new descriptor (the host writes the descriptor, then the tag, then
-            // the doorbell; x86 keeps that order).  Two separate 8-byte reads could tear.
-            // The two polls read different lines (`cmd` / `cmd_b`, slots 0-63 / their copy after the last
-            // slot): a read of a line that is already being read waits for the first to return, so polls
-            // of one line would sample the doorbell only once per round trip.
-            const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)L.descs, (short)0, (int)((XSK_GPU_LOWLAT_MAX + kTile) * sizeof(xsk_gpu_desc)), kRsrcFlags);
-            constexpr int kSysCoherent = 1 | 16;  // cache policy SC0 | SC1
-            static_assert(kPollCopies == 2, "the loop below alternates two copies");
-            auto issue = [&](int copy, uint64_t& c, uint64_t& d0, uint64_t& d1) {
-                c = __hip_atomic_load((uint64_t*)(copy ? &bell->cmd_b : &bell->cmd), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
-                if (leader) {
-                    const int dofs = (int)((copy ? XSK_GPU_LOWLAT_MAX : 0u) * sizeof(xsk_gpu_desc) + lane * 16u);
-                    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(drs, dofs, 0, kSysCoherent);
-                    d0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
-                    d1 = (uint64_t)d.z | ((uint64_t)d.w << 32);
-                }
-            };
-            // 0: keep polling, 1: a batch for this workgroup, 2: leave
-            auto examine = [&](uint64_t cv, uint64_t d0, uint64_t d1) -> int {
-                ++it;
-                const uint64_t c = ((uint64_t)uniform((uint32_t)(cv >> 32)) << 32) | uniform((uint32_t)cv);
-                tr = (wall_clock64() - t_loop) / it;  // mean sampling interval so far
-                if ((uint32_t)c != served) {
-                    const uint32_t nn = (uint32_t)(c >> 32) & 0xFFFFu;
-                    uint32_t w = (uint32_t)(c >> 56) & 7u;
-                    w = w < 1u ? 1u : (w > XSK_GPU__LL_WG ? XSK_GPU__LL_WG : w);
-                    if (g >= w) {  // not serving this batch
-                        served = (uint32_t)c;
-                        return 0;
-                    }
-                    if (leader && w == 1u && nn <= (uint32_t)kTile) {
-                        if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) {
-                            ++n_stale;
-                            return 0;  // not yet
-                        }
-                        sm.desc[lane] = u32x4{(uint32_t)d0, (uint32_t)(d0 >> 32), (uint32_t)d1, (uint32_t)(d1 >> 32)};
-                        dl = 1;
-                    }
-                    uint32_t f1 = 0;
-                    xsk_gpu__ll_slice(nn > XSK_GPU_LOWLAT_MAX ? XSK_GPU_LOWLAT_MAX : nn, w, g, &f0, &f1);
-                    n = f1 - f0;
-                    recs = (uint32_t)(c >> 48) & 1u;
-                    tq = (uint32_t)(c >> 49) & 0x7Fu;
-                    served = (uint32_t)c;
-                    work = 1;
-                    return 1;
-                }
-                if (c & XSK_GPU__BELL_STOP) return 2;
-                if (!leader) {  // the leader's idle exit takes every workgroup of this launch with it
-                    if (__hip_atomic_load(&L.diag->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L.gen)
-                        return 2;
-                } else if (wall_clock64() - t0 > kIdleTicks) {
-                    // leaving: clear `alive`, then look once more (the host posts, then reads `alive`)
-                    __hip_atomic_store((uint32_t*)&bell->wg[0].alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-                    const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
-                                                          __HIP_MEMORY_SCOPE_SYSTEM);
-                    if (uniform((uint32_t)c2) == served || (uniform((uint32_t)(c2 >> 32)) & 0x80000000u)) {
-                        __hip_atomic_store(&L.diag->exit_gen, L.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        return 2;
-                    }
-                    st_sys(&bell->wg[0].alive, 1u);
-                    t0 = wall_clock64();
-                }
-                return 0;
-            };
-            issue(0, cA, aA, bA);
-            __builtin_amdgcn_s_sleep(22);  // ~0.6 us: half a round trip
-            while (true) {
-                issue(1, cB, aB, bB);
-                int r = examine(cA, aA, bA);  // waits for A only (B is still in flight)
-                if (r) break;
-                issue(0, cA, aA, bA);
-                r = examine(cB, aB, bB);
-                if (r) break;
-            }
-            // ONE system-scope acquire for the workgroup: fresh descriptors and frames.  The doorbell read it
-            // follows has returned (it was examined).  The invalidation completes asynchronously and only
-            // this wave's own later loads are ordered behind it, so the wave waits for it (and for the other
-            // poll, still in flight: at most half a round trip) before the barrier below releases the
-            // other waves' loads (MI355X_MICROARCH.md, cross-CU hand-off recipe).
-            if (work) asm volatile("buffer_inv sc0 sc1\n\ts_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) {
-                s_cmd[0] = work;
-                s_cmd[1] = n;
-                s_cmd[2] = recs | (tq << 8) | (dl << 16);
-                s_cmd[3] = f0;
-            }
-            t_seen = wall_clock64();
-            t_poll = tr;
-            n_polls += it;
-            ++n_batches;
+            if (leader) poll_doorbell<true>(L, sm.desc, s_cmd, P, g, lane);
+            else poll_doorbell<false>(L, sm.desc, s_cmd, P, g, lane);
         }
         // the command travels through the LDS only: an LDS-only barrier (__syncthreads() would first wait
         // for wave 0's poll still in flight)
@@ -230,7 +245,9 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         const uint32_t ntiles = (n + tl - 1) / tl;
         if (ntiles)
             echo6_body<kLLTPW, kLLSync, WIRE, true, true, true, false, WIRE ? kWireHeavy : kRefHeavy>(a, 0u, ntiles, sm);
-        asm volatile("" ::"v"(cA), "v"(aA), "v"(bA), "v"(cB), "v"(aB), "v"(bB));
+        // the two polls' registers live across the body: a batch is taken while the other poll is still in
+        // flight, and registers the compiler reused would first have to wait for it to land
+        asm volatile("" ::"v"(P.cA), "v"(P.aA), "v"(P.bA), "v"(P.cB), "v"(P.aB), "v"(P.bB));
         const uint64_t t_rel = wall_clock64();
         const uint64_t c_rel = __builtin_amdgcn_s_memtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have reached the L2 / fabric
@@ -245,20 +262,20 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             // tests/test_lowlat_isa.py checks this sequence in the built code object.
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint64_t t_end = wall_clock64();
-            __hip_atomic_store((uint32_t*)&bell->wg[g].done, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store((uint32_t*)&bell->wg[g].done, P.served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (leader) {  // plain stores to device memory: no wait here, acknowledged long before the next poll
                 xsk_gpu__lldiag* dg = L.diag;
-                dg->trace[0] = t_poll;
-                dg->trace[1] = t_body - t_seen;
+                dg->trace[0] = P.t_poll;
+                dg->trace[1] = t_body - P.t_seen;
                 dg->trace[2] = t_rel - t_body;
                 dg->trace[3] = t_end - t_rel;
                 for (int k = 0; k < 5; ++k) dg->body[k] = s_trace[k];
                 dg->body[5] = t_body;
                 dg->clk[0] = c_rel - c_body;
                 dg->clk[1] = t_rel - t_body;
-                dg->polls[0] = n_batches;
-                dg->polls[1] = n_polls;
-                dg->polls[2] = n_stale;
+                dg->polls[0] = P.n_batches;
+                dg->polls[1] = P.n_polls;
+                dg->polls[2] = P.n_stale;
             }
         }
     }
@@ -323,6 +340,15 @@ void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll) {
 }
 
 int xsk_gpu__lowlat_broken(xsk_gpu__lowlat* ll) { return ll && ll->st.broken; }
+
+int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll) {
+    if (!ll || !ll->st.broken) return 1;
+    (void)hipSetDevice(ll->device);
+    if (!ll_stream_idle(ll)) return 0;
+    ll->st.broken = 0;
+    ll->st.launched = 0;
+    return 1;
+}
 
 static void ll_free(xsk_gpu__lowlat* ll) {
     if (!ll) return;
