@@ -146,7 +146,7 @@ struct xsk_gpu_rec {
 /* ------------------------------------------------------------------------------------------ */
 
 /* Bytes of device workspace xsk_gpu_echo_dev() needs for a batch of n frames on `device`
- * (per-workgroup counter partials; 32 B per 256 frames, at most 512 KiB). */
+ * (per-workgroup counter partials; 32 B per 64-frame tile, at least 512 B, at most 32 KiB). */
 size_t xsk_gpu_workspace_size(int device, uint32_t n);
 
 /* Transform n frames in place on the current HIP device.

@@ -483,6 +483,16 @@ def test_product_kernel_geometries(grid, len_hi, opts):
     _check_grid(umem, descs, grid, opts)
 
 
+@pytest.mark.parametrize("opts", [0, 7])
+@pytest.mark.parametrize("grid", [1, 2, 5, 16])
+@pytest.mark.parametrize("n", [1, 64, 301, 1024])
+def test_small_batch_workgroups(n, grid, opts):
+    """Small batches (n <= XSK_GPU_LOWLAT_MAX: sub-tiles) spread over 1-16 workgroups (the tools/smallbatch.py
+    geometries): every byte, verdict, record and counter exact in reference and wire mode."""
+    umem, descs = _shifted_mixed_batch(n, 2048 + 16, 1500, 0x5EED3030 + n)
+    _check_grid(umem, descs, grid, opts)
+
+
 @pytest.mark.parametrize("flen", [20, 33, 42, 63, 64, 100, 256, 300, 769, 1024, 1500, 4000, 9000])
 def test_uniform_tile_streams(flen):
     """Tiles whose frames all share one length and one 16-B offset (the uniform long-tile stream: byte masks

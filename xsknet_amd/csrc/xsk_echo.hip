@@ -46,6 +46,8 @@ __global__ __launch_bounds__(1024) void fold_counters_kernel(const unsigned long
 
 thread_local const char* g_last_error = "ok";
 
+constexpr uint32_t kSmallWG = 16;  // workgroups a small batch's sub-tiles may spread over
+
 // ---- kernel timing (bench instrumentation) -------------------------------------------------------
 // Events are created per device, lazily, on the device of the launch they bracket; a slot is claimed
 // only once its start event has been recorded.
@@ -116,10 +118,11 @@ const char* xsk_gpu_last_error(void) { return g_last_error; }
 
 size_t xsk_gpu_workspace_size(int device, uint32_t n) {
     if (device < 0) return 0;
-    // room for the partial rows of the round kernel's grid (<= one workgroup per CU)
+    // room for the partial rows of the round kernel's grid (<= one workgroup per CU), or of a small batch's
+    // sub-tiles (<= kSmallWG workgroups)
     const uint32_t ntiles = (n + kTile - 1) / kTile;
     uint32_t g = ntiles < kMaxCuBound ? ntiles : kMaxCuBound;
-    if (g < 1) g = 1;
+    if (g < kSmallWG) g = kSmallWG;
     return (size_t)g * 4 * sizeof(unsigned long long);
 }
 
@@ -156,16 +159,23 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     const uint32_t ncu = xsk_gpu__num_cu(device);
     if (!ncu) return xsk_gpu__hip_fail(hipErrorInvalidDevice);
     uint32_t grid = 0, tiles_per_wg = 0;
-    // a small batch (the RX loop's) runs on ONE workgroup as sub-tiles of ceil(n / 16) frames, so all 16
-    // waves share it: over PCIe (zerocopy host UMEM) one wave alone would stream its 64 frames with only
-    // its own loads in flight
+    // a small batch (the RX loop's) runs as sub-tiles, one per wave, instead of 64-frame tiles: over PCIe
+    // (zerocopy host UMEM) one wave alone would stream its 64 frames with only its own loads in flight, and in
+    // HBM a 64-frame tile per CU leaves the batch's latency to one wave
     const bool small = n <= (uint32_t)XSK_GPU_LOWLAT_MAX;
     uint32_t tl = kTile;
     if (small) {
-        tl = tile ? ((tile + 3u) & ~3u) : ((n + kWaves6 - 1) / kWaves6 + 3u) & ~3u;
+        // sub-tiles of tl frames, one per wave, over up to kSmallWG workgroups of 16 waves: a device-resident
+        // batch on every one of them (tl = ceil(n / 256), >= 4: tools/smallbatch.py measured 1024 x 1500 B in
+        // 14.6 us over 16 workgroups against 44.1 us on one); a zerocopy batch with the caller's tile (about
+        // 8 KiB of PCIe reads per wave, xsk_gpu__small_tile_w), 16 waves per workgroup
+        tl = tile ? ((tile + 3u) & ~3u)
+                  : ((n + kWaves6 * (grid_force ? grid_force : kSmallWG) - 1) /
+                         (kWaves6 * (grid_force ? grid_force : kSmallWG)) + 3u) & ~3u;
         tl = tl < 4u ? 4u : (tl > (uint32_t)kTile ? (uint32_t)kTile : tl);
-        grid = 1;
-        tiles_per_wg = (n + tl - 1) / tl;
+        const uint32_t nt = (n + tl - 1) / tl;
+        tiles_per_wg = grid_force ? (nt + grid_force - 1) / grid_force : (uint32_t)kWaves6;
+        grid = (nt + tiles_per_wg - 1) / tiles_per_wg;
     } else {
         echo6_geometry(n, grid_force ? grid_force : ncu, &grid, &tiles_per_wg);
     }
@@ -195,12 +205,12 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     const int slot = timer_begin(device, s);
     if (opts == 0 && !small)
         echo_round_kernel<false, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    else if (opts == 0)  // one round of sub-tiles, writes as soon as a wave has read
-        echo_round_kernel<false, true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+    else if (opts == 0)  // rounds of sub-tiles, writes as soon as a wave has read
+        echo_round_kernel<false, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (!small)  // wire mode: 128-B windows, one tile per wave per round
         echo_round_kernel<true, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else
-        echo_round_kernel<true, true><<<dim3(1), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
+        echo_round_kernel<true, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     const hipError_t le = hipGetLastError();
     timer_end(slot, s);
     if (le != hipSuccess) return xsk_gpu__hip_fail(le);
@@ -232,9 +242,10 @@ int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem_size, const str
                        tile);
 }
 
-// Internal (tests / tools, not in include/xsk_gpu.h): xsk_gpu_echo_dev_opts with the workgroup count of a
-// large batch forced to `grid` (0 = one per CU), so that shares of several rounds -- paired short tiles,
-// uniform and ranked streams in every round of a share -- run on small batches too.
+// Internal (tests / tools, not in include/xsk_gpu.h): xsk_gpu_echo_dev_opts with the workgroup count forced to
+// `grid` (0 = the default: one per CU for a large batch, one for a small one), so that shares of several rounds --
+// paired short tiles, uniform and ranked streams in every round of a share -- run on small batches too, and small
+// batches' sub-tiles can be spread over several workgroups (tools/smallbatch.py).
 int xsk_gpu__echo_dev_grid(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                            uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                            void* d_workspace, void* stream, uint32_t grid) {

@@ -244,7 +244,7 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
     if (zerocopy(c)) { /* descriptors in, verdicts and counters out: mapped host memory */
         memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
         memset(&c->h_stats[ci], 0, sizeof c->h_stats[ci]);
-        const uint32_t tile = n <= XSK_GPU_LOWLAT_MAX ? xsk_gpu__small_tile(descs + i0, n) : 0u;
+        const uint32_t tile = n <= XSK_GPU_LOWLAT_MAX ? xsk_gpu__small_tile_w(descs + i0, n, 256u) : 0u;
         rc = xsk_gpu__echo_dev_opts_hoststats(c->d_umem, c->umem_size, c->m_descs + i0, n, c->opts, c->m_verd + i0,
                                               want_recs ? c->d_recs + i0 : NULL, c->m_stats + ci, c->d_ws[s], st, tile);
         if (rc) goto out;

@@ -29,23 +29,29 @@ XSK_GPU__HIDDEN int xsk_gpu__echo_dev_opts_hoststats(void* d_umem, uint64_t umem
                                                      uint32_t tile);
 
 /* xsk_echo.hip (exported for tests and tools, not part of the ABI): xsk_gpu_echo_dev_opts with the workgroup
- * count of a large batch (n > XSK_GPU_LOWLAT_MAX) forced to `grid` (0 = one per CU). */
+ * count forced to `grid` (0 = default): a large batch on `grid` static shares, a small one (n <=
+ * XSK_GPU_LOWLAT_MAX) as sub-tiles over `grid` workgroups. */
 int xsk_gpu__echo_dev_grid(void* d_umem, uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
                            uint32_t opts, uint8_t* d_verdicts, struct xsk_gpu_rec* d_recs, struct xsk_gpu_stats* d_stats,
                            void* d_workspace, void* stream, uint32_t grid);
 
 /* Frames per wave for a small batch (n <= XSK_GPU_LOWLAT_MAX) whose frames are read across PCIe: about
- * 8 KiB of frame bytes per wave, 1..16 waves (a 64-frame batch of minimum-size frames is one wave: its
- * few PCIe reads are better in one wave's hands than queued behind sixteen; 1500-B frames spread over
- * every wave).  A multiple of 4 in [4, 64]. */
-static inline uint32_t xsk_gpu__small_tile(const struct xsk_gpu_desc* descs, uint32_t n) {
+ * 8 KiB of frame bytes per wave, 1..max_waves waves (a 64-frame batch of minimum-size frames is one wave: its
+ * few PCIe reads are better in one wave's hands than queued behind many; 1500-B frames spread over as many
+ * waves as their bytes ask for).  A multiple of 4 in [4, 64].  The LOWLAT kernel asks for at most its 16
+ * waves, a launched zerocopy batch for up to 256 (16 workgroups: one CU's loads in flight cap a batch's PCIe
+ * rate). */
+static inline uint32_t xsk_gpu__small_tile_w(const struct xsk_gpu_desc* descs, uint32_t n, uint32_t max_waves) {
     uint64_t bytes = 0;
     for (uint32_t i = 0; i < n; i++) bytes += descs[i].len < 4096u ? descs[i].len : 4096u;
     uint64_t waves = (bytes + 8191u) / 8192u;
-    waves = waves < 1 ? 1 : (waves > 16 ? 16 : waves);
+    waves = waves < 1 ? 1 : (waves > max_waves ? max_waves : waves);
     uint32_t t = (uint32_t)((n + waves - 1) / waves);
     t = (t + 3u) & ~3u;
     return t < 4u ? 4u : (t > 64u ? 64u : t);
+}
+static inline uint32_t xsk_gpu__small_tile(const struct xsk_gpu_desc* descs, uint32_t n) {
+    return xsk_gpu__small_tile_w(descs, n, 16u);
 }
 
 /* xsk_gpu_multi.c: fold the G shares of one xsk_gpu_multi_process call into the caller's counters, all or
