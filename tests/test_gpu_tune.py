@@ -205,3 +205,35 @@ def test_wire_tuning_variants(variant, grid):
     assert (d_umem.cpu().numpy() == ref).all()
     part = ws[:grid * 32].cpu().numpy().view(np.uint64).reshape(grid, 4).sum(axis=0)
     assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("grid", [0, 1, 3])
+def test_product_switch_variants(variant, grid):
+    """The product kernel's source at alternative switch values (tune/xsk_tune_product.hip, the A/B candidates of
+    tools/abbench.py's 1000 + v) on ragged mixed traffic at odd starts, shares of many rounds: every byte, verdict,
+    record and counter partial exact against the oracle (reference mode for 0 / 1, wire mode with every option for
+    2 / 3)."""
+    dev = _dev()
+    L = X.tune_lib()
+    from tests.test_gpu_parity import _shifted_mixed_batch
+    umem, descs = _shifted_mixed_batch(9000, 2048 + 16, 1500, 0x5EED3232 + variant)
+    ref = umem.copy()
+    opts = X.OPT_ALL if variant >= 2 else 0
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
+    d_umem, d_descs = to_dev(umem), to_dev(descs)
+    n = len(descs)
+    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    rc = L.xsk_gpu__product_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                    d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (d_verd.cpu().numpy() == v_ref).all()
+    assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+    assert (d_umem.cpu().numpy() == ref).all()
+    g = int((ws[:1 << 15].cpu().numpy().view(np.uint64).reshape(-1, 4).sum(axis=1) != 0).sum())
+    part = ws[:g * 32].cpu().numpy().view(np.uint64).reshape(g, 4).sum(axis=0)
+    assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
