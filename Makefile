@@ -17,7 +17,8 @@ all: $(LIB) $(TUNELIB) oracle tools/echo_replay
 DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
 # build id of the transform kernel: a hash of the sources that define it and of the flags, reported by
 # xsk_gpu_build_id() so bench.py attaches a PMC traffic summary only to the build it was measured on
-BUILD_ID := $(shell cat $(CSRC)/xsk_echo.hip $(DEVHDR) | sha256sum | cut -c1-16)-$(shell echo '$(HIPFLAGS)' | sha256sum | cut -c1-4)
+# (the device code and its launch: not include/xsk_gpu.h, whose comments change more often than its structs)
+BUILD_ID := $(shell cat $(CSRC)/xsk_echo.hip $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h | sha256sum | cut -c1-16)-$(shell echo '$(HIPFLAGS)' | sha256sum | cut -c1-4)
 HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_lowlat.o
 HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o
 TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o $(CSRC)/tune/xsk_tune_product.o

@@ -208,3 +208,37 @@ def test_multi_status_validation_without_gpu():
     L = X.lib()
     st = (C.c_int * 4)()
     assert L.xsk_gpu_multi_status(None, st, 4) == -errno.EINVAL
+
+
+def test_bench_kernel_names_are_the_shipped_kernels():
+    """bench.py attributes roofline numbers and PMC summaries to KERNEL / WIRE_KERNEL by rocprofv3's demangled
+    name: both must be kernels that libxsknet_amd.so's gfx950 code object really contains."""
+    import sys
+    from tests.test_lowlat_isa import LLVM, gfx950_code_objects
+    import shutil
+    filt = shutil.which("c++filt") or (f"{LLVM}/llvm-cxxfilt" if os.path.exists(f"{LLVM}/llvm-cxxfilt") else None)
+    if not filt:
+        pytest.skip("no demangler (c++filt / llvm-cxxfilt)")
+    sys.path.insert(0, ROOT)
+    import bench
+    import tempfile
+    import xsknet_amd as X
+    names = set()
+    with tempfile.TemporaryDirectory() as td:
+        for k, co in enumerate(gfx950_code_objects(X.LIB_PATH)):
+            p = os.path.join(td, f"co{k}.o")
+            open(p, "wb").write(co)
+            syms = subprocess.run([f"{LLVM}/llvm-readelf", "-s", "-W", p], capture_output=True, text=True,
+                                  check=True).stdout
+            for line in syms.splitlines():
+                f = line.split()
+                if len(f) >= 8 and f[3] == "FUNC":
+                    names.add(subprocess.run([filt, f[7]], capture_output=True, text=True,
+                                             check=True).stdout.strip())
+    short = set()
+    for nm in names:
+        m = re.match(r"^(?:void )?(?:[\w:() ]+::)?(\w+<[^()]*>)\(", nm)
+        if m:
+            short.add(m.group(1))
+    assert bench.KERNEL in short, sorted(short)
+    assert bench.WIRE_KERNEL in short, sorted(short)

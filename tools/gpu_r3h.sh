@@ -1,6 +1,6 @@
-# Round 3: RMETA (rank-ordered step metadata in the ranked streams) A/B against the shipped kernel; tests.
+# Round 3: ROLL (rolled tile loop: 46 KB of kernel code instead of 78 KB) A/B against the shipped kernel; tests.
 cd "$GRAFT_REPO_ROOT" || exit 3
-O=gpurun_out/r3g; mkdir -p $O
+O=gpurun_out/r3h; mkdir -p $O
 export TMPDIR=/tmp
 run() { local name=$1 to=$2; shift 2
   echo "== $name $(date +%T)"; timeout -k 10 "$to" "$@" > "$O/$name.log" 2>&1; local rc=$?

@@ -2,8 +2,10 @@
 // compiles) at alternative values of its remaining template switches, for in-process A/B against the shipped
 // instance (tools/abbench.py variants >= 1000, bench.py --variant).  Tuning library only.
 //   0  as shipped (reference mode)            2  wire mode as shipped (every option)
-//   1  RMETA: ranked streams read their step's metadata rows in rank order (one LDS read per step, not two)
-//   3  wire mode with RMETA
+// (round 3 also measured RMETA -- ranked streams reading their step's metadata rows in rank order, one LDS read
+// per step instead of two dependent ones: c4 195.5 vs 187.2 us, profiles/r03/ab_rank_ordered_meta_*.log -- and
+// ROLL, the tiles of a round in a rolled loop so the kernel's code shrinks from 78 to 46 KB: c4 185.9 vs 185.9 us,
+// c3 275.8 vs 276.0, profiles/r03/ab_rolled_tile_loop_*.log; neither shipped.  New candidates get the free slots.)
 // (round 3 measured RAGGED 2 here -- ragged tiles with their ICMP masks computed once per frame -- against the
 // shipped ranked streams: c4 193.0 vs 185.7 us, profiles/r03/ab_ragged_masks_once_*.log; not shipped)
 #include <errno.h>
@@ -37,9 +39,7 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
     const dim3 gg(grid), bb(kThreads6);
     switch (variant) {
         case 0: echo_round_kernel<false, false><<<gg, bb, 0, s>>>(args, per); break;
-        case 1: echo_round_kernel<false, false, true><<<gg, bb, 0, s>>>(args, per); break;
         case 2: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false><<<gg, bb, 0, s>>>(args, per); break;
-        case 3: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, true><<<gg, bb, 0, s>>>(args, per); break;
         default: return -EINVAL;
     }
     HIP_TRY(hipGetLastError());

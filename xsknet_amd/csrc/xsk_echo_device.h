@@ -265,16 +265,12 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
 // one round trip instead of paying one per step).  The IPv4 header sum is taken in the header phase from
 // the LDS window.  SKM (reference mode): tiles of frames <= 7 row-loads are ranked by counting (one
 // ballot per value), and blocks past row 0 are masked only where one of the slot's frames ends.
-// RMETA: the metadata rows are permuted into rank order (the frame's lane in the packed word's iphi byte, which
-// the ranked streams do not use), so a step's frames cost one LDS read instead of two dependent ones.
-template <int U, bool FAST, bool WIRE, bool SKM, bool RMETA = false>
+template <int U, bool FAST, bool WIRE, bool SKM>
 __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
-                                                   FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
+                                                   const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
                                                    uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
     constexpr uint32_t kRowW = WIRE ? (uint32_t)kWireWin : (uint32_t)kWin;  // LDS row (window) bytes
     const uint32_t q = lane >> 4, k = lane & 15u;
-    FrameMeta6 own;
-    if (RMETA) own = meta[lane];
     uint32_t rank = 0;
     if (SKM && __ballot(nit_own > 7u) == 0ull) {
         // counting rank: per value v one ballot; rank = lanes with fewer row-loads + lanes below with as
@@ -294,14 +290,7 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
             rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
         }
     }
-    if (RMETA) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every lane has its own row before any is overwritten
-        __builtin_amdgcn_wave_barrier();
-        own.packed = (own.packed & ~0xFF00u) | (lane << 8);
-        meta[rank] = own;                                     // meta[r]: the frame of rank r, its lane inside
-    } else {
-        sort[rank] = lane;                                    // sort[0..63]: frame of rank r
-    }
+    sort[rank] = lane;                                    // sort[0..63]: frame of rank r
     if ((rank & 3u) == 3u) sort[64u + (rank >> 2)] = nit_own;  // sort[64 + s]: row-loads of step s
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -331,14 +320,8 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
             v[u] = u32x4{0u, 0u, 0u, 0u};
             if (us[u] < 16u && us[u] != cs) {  // uniform: this slot starts a new step -> its rows' metadata
                 cs = us[u];
-                FrameMeta6 fm;
-                if (RMETA) {
-                    fm = meta[4u * cs + q];
-                    cf = (fm.packed >> 8) & 0xFFu;
-                } else {
-                    cf = sort[4u * cs + q];
-                    fm = meta[cf];
-                }
+                cf = sort[4u * cs + q];
+                const FrameMeta6 fm = meta[cf];
                 crel = fm.rel;
                 clim = fm.lim;
                 crowhi = fm.rowhi;
@@ -866,7 +849,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // within 128 B) are read by 8-lane groups, uniform long tiles (c3, c5) take masks computed once per tile,
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
-template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, bool RMETA = false>
+template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1045,8 +1028,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     } else if (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                uniform(max_nit_lane(nit)) < (uint32_t)U) {
                         // ragged tile (or one too short to fill a batch of U row-loads): ranked streams
-                        if (fast) stream_tile_sorted<U, true, WIRE, REF, RMETA>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
-                        else stream_tile_sorted<U, false, WIRE, REF, RMETA>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        if (fast) stream_tile_sorted<U, true, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<U, false, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
                         stream_tile_uniform<U, WIRE>(ld.r, meta, rows, sums_ic, uniform(nit),
                                                      WIRE ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
@@ -1162,7 +1145,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
-template <bool WIRE, bool SUBT, bool RMETA = false>
+template <bool WIRE, bool SUBT>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1170,7 +1153,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, RMETA>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
