@@ -298,6 +298,27 @@ def host_inclusive(cfg, dev_index):
     return out
 
 
+def reduce_ranks(rank, world, local, *, wall, ev_ms, ok, frames, frame_bytes, kern_avg_ms, launch_bytes, reduce):
+    """The cross-rank step of the bench: max of the timed region (wall clock, events), sums of the frames, bytes
+    and verification flags, and every rank's own figures gathered into rank 0's line (slot r of a zeroed vector,
+    summed).  `reduce(vals, op)` all-reduces a list of floats ("max" / "sum"); the only collectives in the bench
+    (no data-path collective: frames are independent, xsk_receive.c:113-190)."""
+    import torch.distributed as _d  # noqa
+    op_max = _d.ReduceOp.MAX if world > 1 else None
+    op_sum = _d.ReduceOp.SUM if world > 1 else None
+    wall_max, ev_max = reduce([float(wall), float(ev_ms)], op_max)
+    ok_all, frames_all, bytes_all = reduce([1.0 if ok else 0.0, float(frames), float(frame_bytes)], op_sum)
+    achieved = launch_bytes / (kern_avg_ms / 1e3) / 1e9 if kern_avg_ms > 0 else 0.0
+    mine = [0.0] * (5 * world)
+    mine[5 * rank:5 * rank + 5] = [kern_avg_ms * 1e3, achieved, float(wall), float(frames), float(local)]
+    flat = reduce(mine, op_sum)
+    per_rank = [{"rank": r, "device": int(flat[5 * r + 4]), "kernel_avg_us": round(flat[5 * r], 2),
+                 "achieved_gbs": round(flat[5 * r + 1], 1), "frac": round(flat[5 * r + 1] / HBM_PEAK_GBS, 4),
+                 "wall_ms": round(flat[5 * r + 2] * 1e3, 3), "frames": int(flat[5 * r + 3])} for r in range(world)]
+    return {"wall_max": wall_max, "ev_max": ev_max, "ok_ranks": ok_all, "frames": frames_all, "bytes": bytes_all,
+            "per_rank": per_rank}
+
+
 def pool_plan(n, stride, free, warmup, steps, cap=0):
     """Batches in the pool (each: n frames at `stride` + n descriptors) and whether a step must re-arm its
     batch inside the timed loop: one fresh batch per step while W + K batches fit in 85 % of the free HBM
@@ -452,27 +473,16 @@ def main():
     torch.cuda.synchronize()
     read_ceiling = batch_bytes * 5 / (e0.elapsed_time(e1) / 1e3) / 1e9
 
-    import torch.distributed as _d  # noqa
-    op_max = _d.ReduceOp.MAX if world > 1 else None
-    op_sum = _d.ReduceOp.SUM if world > 1 else None
-    wall_max, ev_max = allreduce([wall, ev_ms], op_max, world, dev)
-    ok_all, frames_all, bytes_all = allreduce([1.0 if ok else 0.0, float(K * n), float(K * frame_bytes)], op_sum,
-                                              world, dev)
-    # every rank's own figures, gathered into rank 0's line (slot r of a zeroed vector, summed)
     kern_avg_ms = kern_ms / max(launches, 1)
+    agg = reduce_ranks(rank, world, local, wall=wall, ev_ms=ev_ms, ok=ok, frames=K * n, frame_bytes=K * frame_bytes,
+                       kern_avg_ms=kern_avg_ms, launch_bytes=frame_bytes,
+                       reduce=lambda vals, op: allreduce(vals, op, world, dev))
+    wall_max, ev_max, ok_all = agg["wall_max"], agg["ev_max"], agg["ok_ranks"]
+    frames_all, bytes_all, per_rank = agg["frames"], agg["bytes"], agg["per_rank"]
     achieved = frame_bytes / (kern_avg_ms / 1e3) / 1e9
-    mine = [0.0] * (5 * world)
-    mine[5 * rank:5 * rank + 5] = [kern_avg_ms * 1e3, achieved, wall, float(K * n), float(local)]
-    per_rank_flat = allreduce(mine, op_sum, world, dev)
 
     if rank == 0:
         value = frames_all / wall_max / 1e6
-        per_rank = [{"rank": r, "device": int(per_rank_flat[5 * r + 4]),
-                     "kernel_avg_us": round(per_rank_flat[5 * r], 2),
-                     "achieved_gbs": round(per_rank_flat[5 * r + 1], 1),
-                     "frac": round(per_rank_flat[5 * r + 1] / HBM_PEAK_GBS, 4),
-                     "wall_ms": round(per_rank_flat[5 * r + 2] * 1e3, 3),
-                     "frames": int(per_rank_flat[5 * r + 3])} for r in range(world)]
         traffic, traffic_src = (None, "none: wire mode is not profiled") if args.opts else \
             traffic_from_profiles(args.config, kernel, X.build_id())
         res = {

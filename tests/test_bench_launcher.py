@@ -178,3 +178,53 @@ def test_c5_pool_plan(world):
         assert pool == 1 and rearm  # 128 GiB: one batch, re-armed every step
     if world == 8:
         assert pool >= 10  # 16 GiB batches
+
+
+def _reduce_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def reduce(vals, op):
+            t = torch.tensor(vals, dtype=torch.float64)
+            dist.all_reduce(t, op=op)
+            return t.tolist()
+        agg = bench.reduce_ranks(rank, world, local=rank, wall=0.1 * (rank + 1), ev_ms=50.0 + rank, ok=True,
+                                 frames=20 * (1 << 20), frame_bytes=20 * 1572864000, kern_avg_ms=0.275 + 0.01 * rank,
+                                 launch_bytes=1572864000, reduce=reduce)
+        q.put((rank, agg))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduce_ranks_gloo_world2():
+    """bench.py's cross-rank step over gloo at world size 2 (the driver's N > 1 runs use RCCL): the slowest rank's
+    wall time, summed frames / bytes / verification, and every rank's kernel time, GB/s and frac in rank 0's line."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_reduce_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a = got[0]
+    assert a == got[1]  # every rank sees the same reduction
+    assert abs(a["wall_max"] - 0.2) < 1e-12 and a["ev_max"] == 51.0 and a["ok_ranks"] == 2.0
+    assert a["frames"] == 2 * 20 * (1 << 20) and a["bytes"] == 2 * 20 * 1572864000
+    pr = a["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1] and [r["device"] for r in pr] == [0, 1]
+    assert [r["kernel_avg_us"] for r in pr] == [275.0, 285.0]
+    assert pr[0]["achieved_gbs"] == round(1572864000 / 275e-6 / 1e9, 1)
+    assert pr[1]["frac"] == round(1572864000 / 285e-6 / 1e9 / 8000.0, 4)
+    assert [r["wall_ms"] for r in pr] == [100.0, 200.0] and pr[1]["frames"] == 20 * (1 << 20)
