@@ -207,13 +207,13 @@ def test_wire_tuning_variants(variant, grid):
     assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
 
 
-@pytest.mark.parametrize("variant", [0, 2, 20, 21, 22, 23, 24, 25, 26, 27])
+@pytest.mark.parametrize("variant", [0, 2])
 @pytest.mark.parametrize("grid", [0, 1, 3])
 def test_product_switch_variants(variant, grid):
     """The product kernel's source at alternative switch values (tune/xsk_tune_product.hip, the A/B candidates of
     tools/abbench.py's 1000 + v) on ragged mixed traffic at odd starts, shares of many rounds: every byte, verdict,
     record and counter partial exact against the oracle (reference mode for 0 / 1, wire mode with every option for
-    2 / 3; 20-23: the balanced kernel, static shares and a claimed pool -- its queue counters must be left zero)."""
+    2 / 3)."""
     dev = _dev()
     L = X.tune_lib()
     from tests.test_gpu_parity import _shifted_mixed_batch
@@ -236,4 +236,3 @@ def test_product_switch_variants(variant, grid):
     assert (d_umem.cpu().numpy() == ref).all()
     part = ws[:1 << 15].cpu().numpy().view(np.uint64).reshape(-1, 4).sum(axis=0)  # every partial row (<= 1024)
     assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
-    assert int(ws[1 << 19:(1 << 19) + 8].cpu().numpy().view(np.uint32).max()) == 0

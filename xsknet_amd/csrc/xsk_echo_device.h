@@ -849,9 +849,9 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // within 128 B) are read by 8-lane groups, uniform long tiles (c3, c5) take masks computed once per tile,
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
-template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, bool CNT_OUT = false>
+template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
-                                           Echo6Smem<TPW, WIRE>& sm, Counters* cnt_out = nullptr) {
+                                           Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     static_assert(SYNC == 0 || SYNC == 2, "write phases: at once (0) or heavy waves wait for the round (2)");
     constexpr int U = kU;
@@ -1138,13 +1138,6 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next round
     }
     if (TRACE && threadIdx.x == 0) a.trace[3] = wall_clock64();  // write phase issued
-    if (CNT_OUT) {  // the caller runs more bodies and stores the sum once
-        cnt_out->rxp += cnt.rxp;
-        cnt_out->rxb += cnt.rxb;
-        cnt_out->txp += cnt.txp;
-        cnt_out->txb += cnt.txb;
-        return;
-    }
     store_counters(a, cnt, sm.cnt, wave, lane);
     if (TRACE && threadIdx.x == 0) a.trace[4] = wall_clock64();  // counters added
 }
