@@ -298,6 +298,51 @@ def host_inclusive(cfg, dev_index):
     return out
 
 
+def multi_devices(world, share_gpu=False):
+    """The GPUs of the multi-GPU host-inclusive leg: one context per rank's GPU (LOCAL_RANK r = cuda:r), or every
+    context on cuda:0 in the one-GPU rehearsal."""
+    return [0] * world if share_gpu else list(range(world))
+
+
+def host_inclusive_multi(cfg, world, budget_s=2.0, n=1 << 18):
+    """The PCIe-inclusive rate of ONE host UMEM served by all of this node's ranks' GPUs (N > 1 runs: the driver's
+    scaling curve), measured by rank 0 after the timed region and every collective: xsk_gpu_multi_* in STAGED mode,
+    descriptor i of a call on GPU i mod G, each GPU copying its share's frames in over its own PCIe link and only the
+    rewritten header bytes back, one host thread per GPU (the reference's one UMEM,
+    xsk_utils.c:132-135).  G = 1 on the same UMEM beside it.  Never the bench value; any failure is recorded, not
+    raised."""
+    import oracle
+    import xsknet_amd as X
+    _, lo, hi, stride, seed, _ = CONFIGS[cfg]
+    devs = multi_devices(world, SHARE_GPU)
+    out = {"frames_per_call": n, "frame_len": [lo, hi], "stride": stride, "mode": "staged", "devices": devs,
+           "note": "one host UMEM, xsk_gpu_multi_process over G GPUs (descriptor i on GPU i mod G), measured by rank "
+                   "0 after the timed region; PCIe-inclusive, never the bench value"
+                   + ("; rehearsal: every context on cuda:0" if SHARE_GPU else "")}
+    try:
+        umem = np.zeros(n * stride, np.uint8)
+        descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi, threads=cpu_share()[0])
+        nbytes = int(descs["len"].sum())
+        for g in sorted({1, len(devs)}):
+            work = umem.copy()
+            with X.MultiContext(work, devs[:g], max_batch=n, mode=X.MODE_STAGED) as ctx:
+                v, _, _ = ctx.process(descs, want_recs=False)  # warm
+                ok = bool((v == X.TX_REPLY).all())
+                reps, t = 0, 0.0
+                while t < budget_s:
+                    oracle.rearm(work, descs, v)  # untimed: the frames are requests again
+                    t0 = time.perf_counter()
+                    v, _, st = ctx.process(descs, want_recs=False)
+                    t += time.perf_counter() - t0
+                    reps += 1
+                    ok = ok and bool((v == X.TX_REPLY).all()) and int(st["tx_packets"]) == n
+            out[f"g{g}"] = {"gpus": g, "mframes_per_s": round(reps * n / t / 1e6, 3),
+                            "gib_per_s": round(reps * nbytes / t / 2**30, 3), "calls": reps, "verified": ok}
+    except Exception as e:  # noqa: BLE001 -- context only: the bench line must not depend on it
+        out["error"] = f"{type(e).__name__}: {e}"
+    return out
+
+
 def reduce_ranks(rank, world, local, *, wall, ev_ms, ok, frames, frame_bytes, kern_avg_ms, launch_bytes, reduce):
     """The cross-rank step of the bench: max of the timed region (wall clock, events), sums of the frames, bytes
     and verification flags, and every rank's own figures gathered into rank 0's line (slot r of a zeroed vector,
@@ -339,6 +384,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also measure the PCIe-inclusive rate")
+    ap.add_argument("--no-host-multi", action="store_true",
+                    help="N > 1: skip rank 0's multi-GPU host-inclusive leg after the timed region")
     ap.add_argument("--pool-cap", type=int, default=0, help="cap the batch pool (rehearsals on a shared GPU)")
     ap.add_argument("--alloc", default="slab", choices=("slab", "separate"),
                     help="batch pool as one device allocation (slab, like one UMEM region) or one per batch")
@@ -523,10 +570,16 @@ def main():
         if args.host_inclusive and world == 1:
             log("[rank 0] host-inclusive ...")
             res["host_inclusive"] = host_inclusive(args.config, local)
-        print(json.dumps(res), flush=True)
     if world > 1:
         import torch.distributed as dist
-        dist.destroy_process_group()
+        dist.destroy_process_group()  # the other ranks leave here: their GPUs are free for rank 0's multi leg
+    if rank == 0:
+        if world > 1 and not args.no_host_multi:
+            log(f"[rank 0] host-inclusive over {world} GPUs ...")
+            del slab, umems, descss  # the batch pool: HBM for the STAGED mirrors
+            torch.cuda.empty_cache()
+            res["host_inclusive_multi"] = host_inclusive_multi(args.config, world)
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -228,3 +228,15 @@ def test_reduce_ranks_gloo_world2():
     assert pr[0]["achieved_gbs"] == round(1572864000 / 275e-6 / 1e9, 1)
     assert pr[1]["frac"] == round(1572864000 / 285e-6 / 1e9 / 8000.0, 4)
     assert [r["wall_ms"] for r in pr] == [100.0, 200.0] and pr[1]["frames"] == 20 * (1 << 20)
+
+
+def test_host_inclusive_multi_devices_and_failure_is_recorded():
+    """N > 1 runs: rank 0's multi-GPU host-inclusive leg uses one context per rank's GPU (every one on cuda:0 in the
+    one-GPU rehearsal) and records a failure in its own field instead of raising -- here there is no GPU, so
+    xsk_gpu_multi_init fails and the bench line would still print."""
+    import bench
+    assert bench.multi_devices(4) == [0, 1, 2, 3]
+    assert bench.multi_devices(3, share_gpu=True) == [0, 0, 0]
+    out = bench.host_inclusive_multi("c3", 2, budget_s=0.05, n=256)
+    assert out["devices"] == [0, 1] and out["frames_per_call"] == 256 and out["mode"] == "staged"
+    assert "error" in out and "g2" not in out
