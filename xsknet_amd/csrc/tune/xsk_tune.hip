@@ -319,6 +319,20 @@ __global__ __launch_bounds__(kThreads, MINW) void echo_kernel(EchoArgs a) {
 
 }  // namespace
 
+// 170-172 (round 3): the shipped kernel's switches (variant 158) in workgroups of NWV = 8 waves, two per CU (half
+// the LDS each), so that one workgroup's round tail and write phase overlap the other's reads on the same CU instead
+// of leaving the CU's loads to the last waves of a 16-wave round.  172: heavy threshold 1024 B.
+template <int NWV, int HV>
+__global__ __launch_bounds__(NWV * 64, 2) void echo_kernel6w(EchoArgs a, uint32_t tiles_per_wg) {
+    __shared__ Echo6Smem<2, false, 2, NWV> sm;
+    static_assert(sizeof(sm) <= 81920, "two workgroups per CU");
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t_begin = blockIdx.x * tiles_per_wg;
+    const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
+    echo6_body<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, false, false, NWV, 0, 1,
+               true, false, false, 0, 0, 0, 2, HV>(a, t_begin, t_end, tiles_per_wg, sm);
+}
+
 extern "C" {
 
 uint32_t xsk_gpu__num_cu(int device);  // xsk_echo.hip
@@ -351,6 +365,13 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
         uint32_t g6 = 0, per = 0;
         echo6_geometry(n, max_grid ? max_grid : xsk_gpu__num_cu(device), &g6, &per);
         const dim3 gg(g6), bb(kThreads6);
+        if (variant >= 170 && variant <= 172) {  // two 8-wave workgroups per CU
+            echo6_geometry(n, 2u * (max_grid ? max_grid : xsk_gpu__num_cu(device)), &g6, &per);
+            if (variant == 172) echo_kernel6w<8, 1024><<<dim3(g6), dim3(512), 0, s>>>(args, per);
+            else echo_kernel6w<8, 512><<<dim3(g6), dim3(512), 0, s>>>(args, per);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }
         if ((variant >= 93 && variant <= 95) || (variant >= 99 && variant <= 102)) {  // queue counters at workspace + 768 KiB: zero, left zero
             if (!d_workspace) return -EINVAL;
             args.queue = (uint32_t*)((uint8_t*)d_workspace + (768u << 10));
