@@ -742,3 +742,17 @@ def test_write_through_across_4gib_regions():
     for i, (s, e) in enumerate(spans):
         got = d_umem[s:e].cpu().numpy()
         assert (got == img[i * span:(i + 1) * span]).all(), i
+
+
+@pytest.mark.parametrize("nbytes", [16, 16 * 1023, 16 * 4097 * 3, (1 << 26) + 16 * 77])
+def test_stream_read_ceiling_reads_every_byte(nbytes):
+    """xsk_gpu_stream_read_dev (the bench's read-ceiling kernel: per-workgroup contiguous shares) loads every 16-B
+    vector exactly once: its sum of dwords equals the host's, for sizes that leave ragged shares and tails."""
+    dev = _dev()
+    rng = np.random.default_rng(nbytes)
+    host = rng.integers(0, 2**32, nbytes // 4, dtype=np.uint32)
+    src = torch.from_numpy(host.view(np.uint8).copy()).to(dev)
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    X.stream_read_dev(src, nbytes, out)
+    torch.cuda.synchronize()
+    assert int(out.item()) & (2**64 - 1) == int(host.astype(np.uint64).sum()) & (2**64 - 1)

@@ -22,9 +22,9 @@ FULL = os.environ.get("XSK_TUNE_TESTS") == "1"
 ALL_VARIANTS = [0, 1, 2, 3, 4, 5, 6, 50, 51, 52, 53, 54, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 74,
                 75, 76, 77, 78, 80, 81, 82, 83, 84, 86, 87, 88, 92, 93, 95, 96, 99, 101, 103, 104, 107, 108, 110, 111,
                 112, 113, 116, 117, 118, 119, 121, 122, 123, 125, 126, 130, 131, 132, 133, 134, 135, 136, 137, 138,
-                144, 146, 151, 152, 153, 154, 155, 156, 157, 158, 159, 163, 164, 165, 166, 170, 172]
-DEFAULT_VARIANTS = [158, 131, 170, 172]  # the lab copy of the shipped kernel; the same with plain write-phase stores;
-# the shipped switches in two 8-wave workgroups per CU
+                144, 146, 151, 152, 153, 154, 155, 156, 157, 158, 159, 163, 164, 165, 166, 170, 172, 173, 174, 175]
+DEFAULT_VARIANTS = [158, 131, 170, 172, 173, 174, 175]  # the lab copy of the shipped kernel; the same with plain write-phase stores;
+# the shipped switches in two 8-wave workgroups per CU, and with U = 2 / 3 / 6
 full_only = pytest.mark.skipif(not FULL, reason="the full tuning sweep runs with XSK_TUNE_TESTS=1")
 
 

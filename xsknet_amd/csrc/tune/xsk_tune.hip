@@ -524,6 +524,10 @@ int xsk_gpu__echo_variant(int variant, uint32_t max_grid, void* d_umem, uint64_t
             case 164: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 1, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
             case 165: echo_kernel6<4, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 2, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
             case 166: echo_kernel6<4, 2, 2, 2, true, false, false, false, false, true, true, true, false, false, 0, 1, false, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            // 173-175 (round 3): the shipped kernel (158) with U = 2 / 3 / 6 row-loads per batch in the streams
+            case 173: echo_kernel6<2, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            case 174: echo_kernel6<3, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
+            case 175: echo_kernel6<6, 2, 2, 2, false, false, false, false, false, true, true, true, false, false, 0, 1, true, false, false, 0, 0, 0, 2, 512><<<gg, bb, 0, s>>>(args, per); break;
             case 112: echo_kernel8<6, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 113: echo_kernel8<8, 8, 4><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;
             case 114: echo_kernel8<6, 8, 4, 0, 2, false, true><<<gg, dim3(kThreads8), 0, s>>>(args, per); break;

@@ -187,20 +187,24 @@ __global__ __launch_bounds__(256) void rearm_kernel(uint8_t* umem, const xsk_gpu
     p[37] = (uint8_t)(x >> 8);
 }
 
-// Read-only streaming ceiling: every byte loaded once with 16-B nontemporal loads.
-__global__ __launch_bounds__(256) void stream_read_kernel(const u32x4* src, uint64_t nvec, unsigned long long* out) {
+// Read-only streaming ceiling: every byte loaded once with 16-B nontemporal loads, in the pattern that measured
+// fastest for a plain read (profiles/r01/read_order_ceilings_*.log: 6.8 TB/s on 1.5 GB): one 16-wave workgroup per
+// CU over a contiguous share, each step four 1-KiB wave-loads per wave (64 KiB per workgroup) in flight.
+__global__ __launch_bounds__(1024, 1) void stream_read_kernel(const u32x4* src, uint64_t nvec, unsigned long long* out) {
+    const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;  // 16-B vectors of this workgroup's share
+    const uint64_t b = (uint64_t)blockIdx.x * per;
+    const uint64_t e = b + per < nvec ? b + per : nvec;
     uint64_t acc = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256u;
-    uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    for (; i + 3 * stride < nvec; i += 4 * stride) {
+    uint64_t i = b + threadIdx.x;
+    for (; i + 3 * 1024 < e; i += 4 * 1024) {
         const u32x4 a0 = __builtin_nontemporal_load(src + i);
-        const u32x4 a1 = __builtin_nontemporal_load(src + i + stride);
-        const u32x4 a2 = __builtin_nontemporal_load(src + i + 2 * stride);
-        const u32x4 a3 = __builtin_nontemporal_load(src + i + 3 * stride);
+        const u32x4 a1 = __builtin_nontemporal_load(src + i + 1024);
+        const u32x4 a2 = __builtin_nontemporal_load(src + i + 2048);
+        const u32x4 a3 = __builtin_nontemporal_load(src + i + 3072);
         acc += (uint64_t)a0.x + a0.y + a0.z + a0.w + a1.x + a1.y + a1.z + a1.w;
         acc += (uint64_t)a2.x + a2.y + a2.z + a2.w + a3.x + a3.y + a3.z + a3.w;
     }
-    for (; i < nvec; i += stride) {
+    for (; i < e; i += 1024) {
         const u32x4 a0 = __builtin_nontemporal_load(src + i);
         acc += (uint64_t)a0.x + a0.y + a0.z + a0.w;
     }
@@ -277,7 +281,7 @@ int xsk_gpu_stream_read_dev(const void* d_src, uint64_t bytes, uint64_t* d_out, 
     HIP_TRY(hipGetDevice(&device));
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-    hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)cus * 8u), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)cus), dim3(1024), 0, (hipStream_t)stream,
                        (const u32x4*)d_src, bytes / 16, (unsigned long long*)d_out);
     HIP_TRY(hipGetLastError());
     return 0;
