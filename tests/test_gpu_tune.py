@@ -208,19 +208,19 @@ def test_wire_tuning_variants(variant, grid):
     assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
 @pytest.mark.parametrize("grid", [0, 1, 3])
 def test_product_switch_variants(variant, grid):
     """The product kernel's source at alternative switch values (tune/xsk_tune_product.hip, the A/B candidates of
     tools/abbench.py's 1000 + v) on ragged mixed traffic at odd starts, shares of many rounds: every byte, verdict,
-    record and counter partial exact against the oracle (reference mode for 0 / 1, wire mode with every option for
-    2 / 3)."""
+    record and counter partial exact against the oracle (0: reference mode as shipped, 2: wire mode with every
+    option, 3 / 4: reference mode with 4 / 8 row-loads per batch in the ranked streams instead of 6)."""
     dev = _dev()
     L = X.tune_lib()
     from tests.test_gpu_parity import _shifted_mixed_batch
     umem, descs = _shifted_mixed_batch(9000, 2048 + 16, 1500, 0x5EED3232 + variant)
     ref = umem.copy()
-    opts = X.OPT_ALL if variant in (2, 3) else 0
+    opts = X.OPT_ALL if variant == 2 else 0
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
     d_umem, d_descs = to_dev(umem), to_dev(descs)
     n = len(descs)

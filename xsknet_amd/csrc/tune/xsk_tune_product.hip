@@ -76,6 +76,10 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
     switch (variant) {
         case 0: echo_round_kernel<false, false><<<gg, bb, 0, s>>>(args, per); break;
         case 2: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false><<<gg, bb, 0, s>>>(args, per); break;
+        // 3 / 4: ranked (ragged-tile) streams with 4 (round 2's) / 8 row-loads per batch instead of kUR = 6 (the
+        // uniform stream keeps kU = 4)
+        case 3: echo_round_kernel<false, false, 4><<<gg, bb, 0, s>>>(args, per); break;
+        case 4: echo_round_kernel<false, false, 8><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

@@ -23,6 +23,8 @@ constexpr uint32_t kMaxLen = 1u << 30;      // build-added descriptor sanity bou
 constexpr int kWaves6 = 16;                 // waves per workgroup (one workgroup per CU)
 constexpr int kThreads6 = kWaves6 * 64;     // 1024
 constexpr int kU = 4;                       // 256-B row-loads in flight per lane in the row streams
+constexpr int kUR = 6;                      // the same for the launched kernel's ranked (ragged-tile) streams:
+                                            // c4 185.4 -> 182.6 us, c3 / p98 unchanged (profiles/r03/ab_ranked_u6_u8_*)
 constexpr int kRefTPW = 2;                  // reference mode: tiles per wave per round (2048 frames per CU)
 constexpr int kRefHeavy = 512;              // reference mode: SYNC 2's heavy-frame threshold (bytes)
 constexpr int kWireHeavy = 1024;            // wire mode: the same
@@ -849,7 +851,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // within 128 B) are read by 8-lane groups, uniform long tiles (c3, c5) take masks computed once per tile,
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
-template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY>
+template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1028,8 +1030,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     } else if (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                uniform(max_nit_lane(nit)) < (uint32_t)U) {
                         // ragged tile (or one too short to fill a batch of U row-loads): ranked streams
-                        if (fast) stream_tile_sorted<U, true, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
-                        else stream_tile_sorted<U, false, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        if (fast) stream_tile_sorted<UR, true, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<UR, false, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
                         stream_tile_uniform<U, WIRE>(ld.r, meta, rows, sums_ic, uniform(nit),
                                                      WIRE ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
@@ -1145,7 +1147,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
-template <bool WIRE, bool SUBT>
+template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1153,7 +1155,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
