@@ -389,7 +389,7 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
 // v_dot2_u32_u16 per dword, two masks and the row reduction.  The sums are plain 32-bit sums of 16-bit halves
 // (< 2^32 for frames <= 64 KiB: 257 blocks x 8 halves x 65535 x 16 lanes); the IPv4 header sum comes from the
 // window in the header phase.  WIRE: 128-B windows, and the stream sums row bytes [128, rowhi) (lo = 128).
-template <int U, bool WIRE>
+template <int U, bool WIRE, bool SPLIT = false>
 __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
                                                     uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
                                                     uint32_t lane) {
@@ -397,22 +397,27 @@ __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc,
     const uint32_t q = lane >> 4, k = lane & 15u;
     const u32x4 mf = range_mask((int)(16u * k), (int)lo, (int)hi);                    // row-load 0
     const u32x4 ml = range_mask((int)(256u * (ns - 1u) + 16u * k), (int)lo, (int)hi);  // row-load ns - 1
+    // SPLIT (the launched kernel since round 3): a step's ns row-loads in equal batches of at most U (c3: 3 + 3
+    // instead of 4 + 2 and two loads past the frame that only cost their issue; 274.4 vs 275.4 us in-process A/B,
+    // profiles/r03/ab_uniform_split_*.log)
+    const uint32_t ub = SPLIT ? (ns + (ns + U - 1) / U - 1) / ((ns + U - 1) / U) : (uint32_t)U;  // wave-uniform
     for (uint32_t s = 0; s < 16u; ++s) {
         const uint32_t f = 4u * s + q;
         const FrameMeta6& fm = meta[f];  // broadcast read: one entry per 16-lane row
         const uint32_t rel = fm.rel, lim = fm.lim;
         uint32_t h = 0;
-        for (uint32_t j0 = 0; j0 < ns; j0 += U) {
+        for (uint32_t j0 = 0; j0 < ns; j0 += ub) {
             u32x4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
+                if (SPLIT && ((uint32_t)u >= ub || j0 + (uint32_t)u >= ns)) break;  // wave-uniform
                 v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ro < lim ? rel + ro : 0x80000000u), 0, kAuxNT);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t j = j0 + (uint32_t)u;  // wave-uniform
-                if (j >= ns) break;
+                if (j >= ns || (SPLIT && (uint32_t)u >= ub)) break;
                 u32x4 x = v[u];
                 if (j == 0u && k < kRowW / 16u) *(u32x4*)(rows + f * kRowW + 16u * k) = x;  // the header window
                 if (j == 0u) x &= mf;
@@ -851,7 +856,8 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // within 128 B) are read by 8-lane groups, uniform long tiles (c3, c5) take masks computed once per tile,
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
-template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU>
+template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
+          bool USPLIT = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1033,7 +1039,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                         if (fast) stream_tile_sorted<UR, true, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                         else stream_tile_sorted<UR, false, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
-                        stream_tile_uniform<U, WIRE>(ld.r, meta, rows, sums_ic, uniform(nit),
+                        stream_tile_uniform<U, WIRE, USPLIT>(ld.r, meta, rows, sums_ic, uniform(nit),
                                                      WIRE ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
                     } else {
                         // every frame the same number of row-loads, but different offsets or ends: per-step streams
@@ -1147,7 +1153,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
-template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR>
+template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1155,7 +1161,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
