@@ -8,6 +8,9 @@
 // c3 275.8 vs 276.0, profiles/r03/ab_rolled_tile_loop_*.log; neither shipped.  New candidates get the free slots.)
 // (round 3 measured RAGGED 2 here -- ragged tiles with their ICMP masks computed once per frame -- against the
 // shipped ranked streams: c4 193.0 vs 185.7 us, profiles/r03/ab_ragged_masks_once_*.log; not shipped)
+// (round 3 measured RLANE -- the uniform stream taking its rows' frame offsets from the owner lanes by readlane
+// instead of one LDS read of the step's metadata: c3 274.2 vs 274.8 and 281.8 vs 281.5 us, within noise,
+// profiles/r03/ab_uniform_rlane*_c3.log; removed)
 // (round 3 measured BAL -- static shares for 15/16 .. 3/4 of the tiles, the rest a pool drained with claims on a
 // device counter in shrinking sub-tile units -- as variants 20-27 of commit a9c3d74: c3 +19 to +60 us, c4 +8 to +48,
 // c2 +11 to +30; profiles/r03/balance/.  Removed: it needed a counter-output switch in the product body.)
