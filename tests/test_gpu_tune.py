@@ -208,20 +208,20 @@ def test_wire_tuning_variants(variant, grid):
     assert [int(v) for v in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("grid", [0, 1, 3])
 def test_product_switch_variants(variant, grid):
     """The product kernel's source at alternative switch values (tune/xsk_tune_product.hip, the A/B candidates of
     tools/abbench.py's 1000 + v) on ragged mixed traffic at odd starts, shares of many rounds: every byte, verdict,
     record and counter partial exact against the oracle (0: reference mode as shipped, 2: wire mode with every
     option, 3 / 4: reference mode with 4 / 8 row-loads per batch in the ranked streams instead of 6, 5 / 6: the uniform
-    stream without SPLIT (batches of 4 and a remainder), reference / wire mode)."""
+    stream without SPLIT (batches of 4 and a remainder), reference / wire mode, 7 / 8: without PRIO, reference / wire)."""
     dev = _dev()
     L = X.tune_lib()
     from tests.test_gpu_parity import _shifted_mixed_batch
     umem, descs = _shifted_mixed_batch(9000, 2048 + 16, 1500, 0x5EED3232 + variant)
     ref = umem.copy()
-    opts = X.OPT_ALL if variant in (2, 6) else 0
+    opts = X.OPT_ALL if variant in (2, 6, 8) else 0
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
     d_umem, d_descs = to_dev(umem), to_dev(descs)
     n = len(descs)
@@ -240,7 +240,7 @@ def test_product_switch_variants(variant, grid):
     assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6])
+@pytest.mark.parametrize("variant", [0, 5, 6, 7, 8])
 @pytest.mark.parametrize("flen", [20, 42, 64, 100, 300, 769, 1024, 1500, 2300, 4000])
 def test_product_switch_uniform_tiles(variant, flen):
     """The product kernel's switches on tiles whose frames share one length and one 16-B offset (the uniform
@@ -250,7 +250,7 @@ def test_product_switch_uniform_tiles(variant, flen):
     dev = _dev()
     n = 64 * 20 + 17  # past XSK_GPU_LOWLAT_MAX: the round kernel's geometry
     stride = ((flen + 16 + 255) // 256) * 256 + 256
-    opts = X.OPT_ALL if variant == 6 else 0
+    opts = X.OPT_ALL if variant in (6, 8) else 0
     for off in (0, 1, 6, 15):
         umem = np.zeros(n * stride + 256, np.uint8)
         descs = oracle.synth_batch(umem, n, 256 + off, stride, seed=0x5EED2121 + flen + off, mode=0, len_lo=flen,

@@ -86,6 +86,9 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         // 5 / 6: the uniform stream's row-loads in batches of 4 and a remainder (round 2's, no SPLIT), reference / wire
         case 5: echo_round_kernel<false, false, kUR, false><<<gg, bb, 0, s>>>(args, per); break;
         case 6: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, false><<<gg, bb, 0, s>>>(args, per); break;
+        // 7 / 8: without PRIO (a stream batch's address work and loads at the default priority), reference / wire mode
+        case 7: echo_round_kernel<false, false, kUR, true, false><<<gg, bb, 0, s>>>(args, per); break;
+        case 8: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, false><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

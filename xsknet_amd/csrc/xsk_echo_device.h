@@ -267,7 +267,7 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
 // one round trip instead of paying one per step).  The IPv4 header sum is taken in the header phase from
 // the LDS window.  SKM (reference mode): tiles of frames <= 7 row-loads are ranked by counting (one
 // ballot per value), and blocks past row 0 are masked only where one of the slot's frames ends.
-template <int U, bool FAST, bool WIRE, bool SKM>
+template <int U, bool FAST, bool WIRE, bool SKM, bool PRIO = false>
 __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
                                                    const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
                                                    uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
@@ -306,6 +306,9 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
     while (s < 16u) {
         u32x4 v[U];
         uint32_t us[U], uj[U], uf[U], urowhi[U], ulim[U], uoff[U];
+        // PRIO (the launched kernel since round 3): the batch's address work and loads ahead of the other waves' VALU
+        // on the SIMD -- c4 185.5 -> 183.5 us, c3 274.7 -> 273.7, c2 35.1 -> 34.8 (profiles/r03/ab_stream_prio_*.log)
+        if (PRIO) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
         for (int u = 0; u < U; ++u) {  // wave-uniform slot assignment
             us[u] = s;
@@ -344,6 +347,7 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
                 }
             }
         }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (us[u] >= 16u) continue;  // uniform
@@ -389,7 +393,7 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
 // v_dot2_u32_u16 per dword, two masks and the row reduction.  The sums are plain 32-bit sums of 16-bit halves
 // (< 2^32 for frames <= 64 KiB: 257 blocks x 8 halves x 65535 x 16 lanes); the IPv4 header sum comes from the
 // window in the header phase.  WIRE: 128-B windows, and the stream sums row bytes [128, rowhi) (lo = 128).
-template <int U, bool WIRE, bool SPLIT = false>
+template <int U, bool WIRE, bool SPLIT = false, bool PRIO = false>
 __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
                                                     uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
                                                     uint32_t lane) {
@@ -408,12 +412,14 @@ __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc,
         uint32_t h = 0;
         for (uint32_t j0 = 0; j0 < ns; j0 += ub) {
             u32x4 v[U];
+            if (PRIO) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
                 if (SPLIT && ((uint32_t)u >= ub || j0 + (uint32_t)u >= ns)) break;  // wave-uniform
                 v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ro < lim ? rel + ro : 0x80000000u), 0, kAuxNT);
             }
+            if (PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t j = j0 + (uint32_t)u;  // wave-uniform
@@ -857,7 +863,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false>
+          bool USPLIT = false, bool PRIO = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1036,10 +1042,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     } else if (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                uniform(max_nit_lane(nit)) < (uint32_t)U) {
                         // ragged tile (or one too short to fill a batch of U row-loads): ranked streams
-                        if (fast) stream_tile_sorted<UR, true, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
-                        else stream_tile_sorted<UR, false, WIRE, REF>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        if (fast) stream_tile_sorted<UR, true, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<UR, false, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
-                        stream_tile_uniform<U, WIRE, USPLIT>(ld.r, meta, rows, sums_ic, uniform(nit),
+                        stream_tile_uniform<U, WIRE, USPLIT, PRIO>(ld.r, meta, rows, sums_ic, uniform(nit),
                                                      WIRE ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
                     } else {
                         // every frame the same number of row-loads, but different offsets or ends: per-step streams
@@ -1153,7 +1159,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
-template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT>
+template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1161,7 +1167,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
