@@ -8,6 +8,9 @@
 // c3 275.8 vs 276.0, profiles/r03/ab_rolled_tile_loop_*.log; neither shipped.  New candidates get the free slots.)
 // (round 3 measured RAGGED 2 here -- ragged tiles with their ICMP masks computed once per frame -- against the
 // shipped ranked streams: c4 193.0 vs 185.7 us, profiles/r03/ab_ragged_masks_once_*.log; not shipped)
+// (round 3 measured RH2 -- the ranked streams summing 16-bit halves with v_dot2 in 32 bits -- and PRIO2 -- also the
+// descriptor, paired-short and short / ping-size loads at s_setprio 2: c4 182.5 / 182.0 vs 182.9 us, c3 274.7 / 275.2
+// vs 274.7, p98 64.0 / 64.6 vs 64.1, within noise, profiles/r03/ab_rh2_prio2_*.log; removed)
 // (round 3 measured RLANE -- the uniform stream taking its rows' frame offsets from the owner lanes by readlane
 // instead of one LDS read of the step's metadata: c3 274.2 vs 274.8 and 281.8 vs 281.5 us, within noise,
 // profiles/r03/ab_uniform_rlane*_c3.log; removed)
