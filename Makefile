@@ -12,7 +12,7 @@ CSRC     := xsknet_amd/csrc
 LIB      := xsknet_amd/libxsknet_amd.so
 TUNELIB  := xsknet_amd/libxsknet_amd_tune.so
 
-all: $(LIB) $(TUNELIB) oracle tools/echo_replay
+all: $(LIB) $(TUNELIB) oracle tools/echo_replay tools/rxqueues
 
 DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h include/xsk_gpu.h
 # build id of the transform kernel: a hash of the sources that define it and of the flags, reported by
@@ -45,11 +45,14 @@ $(TUNELIB): $(TUNEOBJ) $(LIB)
 tools/echo_replay: tools/echo_replay.c $(LIB) include/xsk_gpu.h
 	$(CC) $(CFLAGS) -o $@ $< -L xsknet_amd -lxsknet_amd -Wl,-rpath,'$$ORIGIN/../xsknet_amd'
 
+tools/rxqueues: tools/rxqueues.c $(LIB) include/xsk_gpu.h
+	$(CC) $(CFLAGS) -o $@ $< -L xsknet_amd -lxsknet_amd -pthread -Wl,-rpath,'$$ORIGIN/../xsknet_amd'
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay
+	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay tools/rxqueues
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

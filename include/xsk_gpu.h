@@ -196,10 +196,23 @@ enum xsk_gpu_mode {
 /* Largest batch the LOWLAT doorbell takes (larger ones are launched). */
 #define XSK_GPU_LOWLAT_MAX 1024u
 
+/* Resident LOWLAT kernels per device in one process.  Each waits for batches on a highest-priority stream of its
+ * own, and the HIP runtime backs a process's streams of one priority with a few hardware queues (GPU_MAX_HW_QUEUES,
+ * 4 by default): a resident kernel that lands on a queue behind another one does not start until that one exits,
+ * and its batches would time out (tools/rxqueues: 8 LOWLAT queues on one GPU, 4 of them -ETIMEDOUT).  A context
+ * created in XSK_GPU_MODE_LOWLAT while XSK_GPU_LOWLAT_PER_DEVICE LOWLAT contexts of this process already exist on
+ * its device runs as XSK_GPU_MODE_ZEROCOPY (same results, a launch per batch); xsk_gpu_ctx_mode() reports the mode
+ * a context runs in.  xsk_gpu_fini() releases the slot. */
+#define XSK_GPU_LOWLAT_PER_DEVICE 4
+
 /* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
  * xsk_utils.c:132-135).  The UMEM is page-locked (hipHostRegister) until xsk_gpu_fini().
  * max_batch bounds n of later calls. */
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode);
+
+/* The mode `ctx` runs in (XSK_GPU_MODE_*): the one it was created with, except a LOWLAT request beyond
+ * XSK_GPU_LOWLAT_PER_DEVICE, which runs as ZEROCOPY.  -EINVAL for NULL. */
+int xsk_gpu_ctx_mode(const xsk_gpu_ctx* ctx);
 
 /* Synchronously process one batch of host descriptors against the bound UMEM.  Same outputs as
  * xsk_gpu_echo_dev(); `verdicts`, `recs` and `stats` are host pointers (each may be NULL).

@@ -23,6 +23,7 @@ def declared_functions():
 def test_header_declares_expected_entry_points():
     fns = declared_functions()
     for f in ("xsk_gpu_echo_dev", "xsk_gpu_init", "xsk_gpu_process", "xsk_gpu_fini", "xsk_gpu_workspace_size",
+              "xsk_gpu_ctx_mode",
               "xsk_gpu_synth_dev", "xsk_gpu_rearm_dev", "xsk_gpu_stream_read_dev", "xsk_gpu_abi_version",
               "xsk_gpu_last_error", "xsk_gpu_timing_enable", "xsk_gpu_timing_read"):
         assert f in fns
@@ -109,6 +110,7 @@ def test_abi_version_and_argument_validation():
     assert L.xsk_gpu_echo_dev_opts(0x1001, 4096, 0x2000, 1, 7, None, None, None, None, None) == EINVAL
     assert L.xsk_gpu_echo_dev_opts(0x1000, 4096, 0x2000, 0xFFFFFFFF, 7, None, None, None, None, None) == EINVAL
     assert L.xsk_gpu_set_options(None, 1) == EINVAL
+    assert L.xsk_gpu_ctx_mode(None) == EINVAL
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 8, 2048, 0, 0, 1, 0, 64, 64, None) == EINVAL
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 32, 0, 0, 1, 0, 64, 64, None) == EINVAL
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 2048, 0, 0, 1, 2, 64, 64, None) == EINVAL

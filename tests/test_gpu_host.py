@@ -351,3 +351,35 @@ def test_multi_lowlat_path_chosen_per_batch():
             for k in tot:
                 tot[k] += int(st[k])
     check(umem, work, descs, np.concatenate(vs), None, tot)
+
+
+def test_lowlat_contexts_per_device_limit():
+    """At most XSK_GPU_LOWLAT_PER_DEVICE resident LOWLAT kernels per device in one process (more would queue behind
+    each other on the runtime's few high-priority hardware queues and time out, tools/rxqueues): further LOWLAT
+    requests run as ZEROCOPY (xsk_gpu_ctx_mode), every context bit-exact on 64-frame RX batches, and fini gives the
+    slots back."""
+    import gc
+    _dev()
+    gc.collect()  # contexts of earlier tests are closed (their slots released)
+    n = 256
+    umems, descss, ctxs = [], [], []
+    try:
+        for q in range(X.LOWLAT_PER_DEVICE + 2):
+            umem = np.zeros(n * 4096, np.uint8)
+            descs = oracle.synth_batch(umem, n, 256, 4096, 0x5EED4040 + q, mode=1, len_lo=20, len_hi=1500)
+            umems.append(umem)
+            descss.append(descs)
+            ctxs.append(X.EchoContext(umem.copy(), 0, max_batch=64, mode=X.MODE_LOWLAT))
+        modes = [c.mode for c in ctxs]
+        assert modes == [X.MODE_LOWLAT] * X.LOWLAT_PER_DEVICE + [X.MODE_ZEROCOPY] * 2, modes
+        for umem, descs, ctx in zip(umems, descss, ctxs):
+            v, r, tot = run_batches(ctx, descs, 64)
+            check(umem, ctx.umem, descs, v, r, tot)
+            ref = umem.copy()
+            oracle.echo_batch(ref, descs)
+            assert (ctx.umem == ref).all()
+    finally:
+        for c in ctxs:
+            c.close()
+    with X.EchoContext(np.zeros(1 << 16, np.uint8), 0, max_batch=64, mode=X.MODE_LOWLAT) as c:
+        assert c.mode == X.MODE_LOWLAT

@@ -42,6 +42,7 @@ F_IP_CSUM_OK, F_ICMP_CSUM_OK, F_VLAN, F_IP_OPTIONS = 1, 2, 4, 8
 MODE_ZEROCOPY, MODE_STAGED, MODE_LOWLAT = 0, 1, 2
 LOWLAT_MAX = 1024  # XSK_GPU_LOWLAT_MAX
 MULTI_MAX = 16  # XSK_GPU_MULTI_MAX
+LOWLAT_PER_DEVICE = 4  # XSK_GPU_LOWLAT_PER_DEVICE
 
 # struct xsk_gpu_desc == struct xdp_desc (linux/if_xdp.h)
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
@@ -100,6 +101,7 @@ _SIGS = {
     "xsk_gpu_init": ([C.POINTER(_P), C.c_int, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
     "xsk_gpu_process": ([_P, _P, C.c_uint32, _P, _P, _P], C.c_int),
     "xsk_gpu_fini": ([_P], None),
+    "xsk_gpu_ctx_mode": ([_P], C.c_int),
     "xsk_gpu_synth_dev": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                            C.c_uint64, C.c_int, C.c_uint32, C.c_uint32, _P], C.c_int),
     "xsk_gpu_rearm_dev": ([_P, _P, _P, C.c_uint32, _P], C.c_int),
@@ -266,6 +268,12 @@ class EchoContext:
 
     def set_options(self, opts: int) -> None:
         _check("xsk_gpu_set_options", lib().xsk_gpu_set_options(self._ctx, opts))
+
+    @property
+    def mode(self) -> int:
+        """xsk_gpu_ctx_mode: the mode the context runs in (a LOWLAT request beyond XSK_GPU_LOWLAT_PER_DEVICE on its
+        device runs as ZEROCOPY)."""
+        return lib().xsk_gpu_ctx_mode(self._ctx)
 
     def process(self, descs: np.ndarray, want_recs: bool = True):
         n = len(descs)

@@ -25,6 +25,7 @@
 #define __HIP_PLATFORM_AMD__ 1
 #include <errno.h>
 #include <hip/hip_runtime_api.h>
+#include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -61,7 +62,24 @@ struct xsk_gpu_ctx {
     hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
     int registered;   /* this context registered the UMEM (and unregisters it at fini) */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
+    int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
 };
+
+/* LOWLAT contexts per device in this process (include/xsk_gpu.h, XSK_GPU_LOWLAT_PER_DEVICE): a slot is taken at
+ * init and given back at fini; a LOWLAT request without a free slot runs as ZEROCOPY. */
+#define LL_MAX_DEV 64
+static atomic_int g_ll_slots[LL_MAX_DEV];
+
+static int ll_slot_take(int device) {
+    if (device < 0 || device >= LL_MAX_DEV) return 0;
+    int cur = atomic_load(&g_ll_slots[device]);
+    while (cur < XSK_GPU_LOWLAT_PER_DEVICE)
+        if (atomic_compare_exchange_weak(&g_ll_slots[device], &cur, cur + 1)) return 1;
+    return 0;
+}
+static void ll_slot_give(int device) {
+    if (device >= 0 && device < LL_MAX_DEV) atomic_fetch_sub(&g_ll_slots[device], 1);
+}
 
 /* ZEROCOPY and LOWLAT read the UMEM in place through its mapped alias */
 static int zerocopy(const xsk_gpu_ctx* c) { return c->mode != XSK_GPU_MODE_STAGED; }
@@ -79,6 +97,7 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    if (c->ll_slot) ll_slot_give(c->device);
     xsk_gpu__lowlat_free(c->ll);
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamSynchronize(c->stream[s]);
@@ -118,6 +137,10 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     if (!c) return -ENOMEM;
     c->device = device;
     c->mode = mode;
+    if (mode == XSK_GPU_MODE_LOWLAT) { /* no free slot: ZEROCOPY, the same data path with a launch per batch */
+        c->ll_slot = ll_slot_take(device);
+        if (!c->ll_slot) c->mode = XSK_GPU_MODE_ZEROCOPY;
+    }
     c->umem = (uint8_t*)umem;
     c->umem_size = umem_size;
     c->max_batch = max_batch;
@@ -162,7 +185,7 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
         goto out;
     }
     for (uint32_t i = 0; i < c->max_chunks; i++) TRY(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
-    if (mode == XSK_GPU_MODE_LOWLAT) {
+    if (c->mode == XSK_GPU_MODE_LOWLAT) {
         rc = xsk_gpu__lowlat_start(&c->ll, c->d_umem, umem_size, 0);
         if (rc) goto out;
     }
@@ -182,6 +205,7 @@ int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t ume
 }
 
 uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* c) { return c ? c->max_batch : 0u; }
+int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
 xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
 
 /* Uniform stride S (>= 64, multiple of 16) when addr[i] = addr[0] + i*S for the whole chunk. */
