@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--variants", default="-1,131")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--pool", type=int, default=0, help="batches in the pool (0: as many as fit, <= 24)")
+    ap.add_argument("--burst", type=int, default=0,
+                    help="sustained regime: each variant runs BURST consecutive launches per round (the bench's back-"
+                         "to-back loop) and only the second half of each burst is counted; 0 = interleave per launch")
     args = ap.parse_args()
     V = [int(v) for v in args.variants.split(",")]
     dev = torch.device("cuda", 0)
@@ -37,7 +40,7 @@ def main():
     bb = n * stride
     free, _ = torch.cuda.mem_get_info(dev)
     pool = args.pool or max(len(V), min(24, int(free * 0.8) // (bb + n * 16) - 1))
-    pool -= pool % len(V)
+    pool -= pool % (len(V) * args.burst if args.burst else len(V))
     slab = torch.empty(pool * bb, dtype=torch.uint8, device=dev)
     descs = [torch.empty(n * 16, dtype=torch.uint8, device=dev) for _ in range(pool)]
     verd = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -73,18 +76,32 @@ def main():
     for r in range(args.rounds):
         regen()
         evs = []
-        for b in range(pool):
-            v = V[(b + r) % len(V)]
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            launch(v, b)
-            e1.record(stream)
-            evs.append((v, e0, e1))
+        if args.burst:  # blocks of `burst` back-to-back launches per variant (the bench's loop), block order rotating
+            half = args.burst // 2
+            for blk in range(pool // args.burst):
+                v = V[(blk + r) % len(V)]
+                b0 = blk * args.burst
+                for b in range(b0, b0 + args.burst - half):  # warms the clock state: not counted
+                    launch(v, b)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for b in range(b0 + args.burst - half, b0 + args.burst):
+                    launch(v, b)
+                e1.record(stream)
+                evs.append((v, e0, e1, half))
+        else:
+            for b in range(pool):
+                v = V[(b + r) % len(V)]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                launch(v, b)
+                e1.record(stream)
+                evs.append((v, e0, e1, 1))
         torch.cuda.synchronize()
-        for v, e0, e1 in evs:
-            times[v].append(e0.elapsed_time(e1) * 1000.0)
-        print(json.dumps({"round": r, **{str(v): round(float(np.median(times[v][-pool // len(V):])), 2) for v in V}}),
-              flush=True)
+        for v, e0, e1, m in evs:  # microseconds per launch (a burst's counted half: its average)
+            times[v].append(e0.elapsed_time(e1) * 1000.0 / m)
+        print(json.dumps({"round": r, **{str(v): round(float(np.median(times[v][-max(1, len(evs) // len(V)):])), 2)
+                                         for v in V}}), flush=True)
     out = {"config": args.config, "pool": pool, "rounds": args.rounds, "desc": desc}
     for v in V:
         t = np.sort(np.array(times[v]))

@@ -12,6 +12,8 @@
 // mod 4), against the 16-way bank conflicts of the per-lane header-phase reads (6.7 M conflict cycles per launch,
 // profiles/r03/lds/): c2 34.7 vs 35.2 us, c3 274.2 vs 275.1, c4 183.4 vs 182.8 against the same kernel without it,
 // profiles/r03/ab_lds_swizzle_stdout.jsonl; within noise, removed)
+// (round 3 measured RH2 again in the sustained regime, tools/abbench.py --burst: c4 179.6 vs 179.8 us shipped, 181.9
+// without PRIO, profiles/r03/ab_burst_prio_rh2_c4.log)
 // (round 3 measured RH2 -- the ranked streams summing 16-bit halves with v_dot2 in 32 bits -- and PRIO2 -- also the
 // descriptor, paired-short and short / ping-size loads at s_setprio 2: c4 182.5 / 182.0 vs 182.9 us, c3 274.7 / 275.2
 // vs 274.7, p98 64.0 / 64.6 vs 64.1, within noise, profiles/r03/ab_rh2_prio2_*.log; removed)
