@@ -21,7 +21,7 @@ DEVHDR   := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip
 BUILD_ID := $(shell cat $(CSRC)/xsk_echo.hip $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h | sha256sum | cut -c1-16)-$(shell echo '$(HIPFLAGS)' | sha256sum | cut -c1-4)
 HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_lowlat.o
 HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o
-TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o $(CSRC)/tune/xsk_tune_product.o
+TUNEOBJ  := $(CSRC)/tune/xsk_tune.o $(CSRC)/tune/xsk_wire_v1.o $(CSRC)/tune/xsk_tune_product.o $(CSRC)/tune/xsk_tune_slack.o
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(DEVHDR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -34,6 +34,13 @@ $(CSRC)/tune/%.o: $(CSRC)/tune/%.hip $(DEVHDR) $(CSRC)/tune/xsk_echo_variants.h 
 
 $(CSRC)/%.o: $(CSRC)/%.c include/xsk_gpu.h $(CSRC)/xsk_gpu_internal.h $(CSRC)/xsk_ring.h
 	$(CC) $(CFLAGS) -pthread -I$(ROCM)/include -c -o $@ $<
+
+# the round-4 candidate SLACK, on a copy of the product header (tune/xsk_tune_slack.hip)
+$(CSRC)/xsk_echo_device_slack.gen.h: $(CSRC)/xsk_echo_device.h tools/slack_header.patch
+	patch -s -o $@ $(CSRC)/xsk_echo_device.h tools/slack_header.patch
+
+$(CSRC)/tune/xsk_tune_slack.o: $(CSRC)/tune/xsk_tune_slack.hip $(CSRC)/xsk_echo_device_slack.gen.h $(DEVHDR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(LIB): $(HIPOBJ) $(HOSTOBJ)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -pthread -Wl,-soname,libxsknet_amd.so
@@ -52,7 +59,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay tools/rxqueues
+	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay tools/rxqueues $(CSRC)/xsk_echo_device_slack.gen.h
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -272,3 +272,33 @@ def test_product_switch_uniform_tiles(variant, flen):
             assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all(), (off, grid)
             assert (d_umem.cpu().numpy() == ref).all(), (off, grid)
             d_umem.copy_(to_dev(umem))
+
+
+@full_only
+@pytest.mark.parametrize("variant", [0, 1, 2, 4])
+@pytest.mark.parametrize("grid", [0, 1, 3])
+def test_slack_candidate_variants(variant, grid):
+    """The round-4 candidate SLACK (tune/xsk_tune_slack.hip: the product kernel built from a patched copy of its header;
+    heavy waves write once all but SLACK waves have read) on ragged mixed traffic at odd starts: every byte, verdict,
+    record and counter partial exact against the oracle (the write-phase wait is a schedule, never a dependency)."""
+    dev = _dev()
+    L = X.tune_lib()
+    from tests.test_gpu_parity import _shifted_mixed_batch
+    umem, descs = _shifted_mixed_batch(9000, 2048 + 16, 1500, 0x5EED3535 + variant)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, 0)
+    d_umem, d_descs = to_dev(umem), to_dev(descs)
+    n = len(descs)
+    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    rc = L.xsk_gpu__slack_variant(variant, grid, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                  d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (d_verd.cpu().numpy() == v_ref).all()
+    assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
+    assert (d_umem.cpu().numpy() == ref).all()
+    part = ws[:1 << 15].cpu().numpy().view(np.uint64).reshape(-1, 4).sum(axis=0)
+    assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]

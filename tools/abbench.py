@@ -59,6 +59,10 @@ def main():
         u = slab[b * bb:(b + 1) * bb]
         if v < 0:
             X.echo_dev(u, descs[b], n, verd, recs, stats, ws, stream)
+        elif v >= 2000:  # the SLACK candidate (tune/xsk_tune_slack.hip)
+            rc = tune.xsk_gpu__slack_variant(v - 2000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
+                                             verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
+            assert rc == 0, rc
         elif v >= 1000:
             rc = tune.xsk_gpu__product_variant(v - 1000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
                                                verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)

@@ -128,6 +128,7 @@ _TUNE_SIGS = {
     "xsk_gpu__echo_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
     "xsk_gpu__echo_wire_variant": ([C.c_int, _P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P], C.c_int),
     "xsk_gpu__product_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
+    "xsk_gpu__slack_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
 }
 _tune: Optional[C.CDLL] = None
 
