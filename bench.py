@@ -31,9 +31,9 @@ import torch  # noqa: E402
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # the transform kernel xsk_gpu_echo_dev launches for a large batch (the name rocprofv3 reports)
-KERNEL = "echo_round_kernel<false, false, 6, true, true>"
+KERNEL = "echo_round_kernel<false, false, 6, true, true, 2>"
 # xsk_gpu_echo_dev_opts, nonzero --opts
-WIRE_KERNEL = "echo_round_kernel<true, false, 6, true, true>"
+WIRE_KERNEL = "echo_round_kernel<true, false, 6, true, true, 0>"
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),
@@ -364,6 +364,12 @@ def reduce_ranks(rank, world, local, *, wall, ev_ms, ok, frames, frame_bytes, ke
             "per_rank": per_rank}
 
 
+def frac_of_ceiling(achieved, read_ceiling):
+    """roofline.frac_of_read_ceiling: the kernel's algorithmic GB/s over the measured plain-read ceiling of the same
+    slab (None when the ceiling was not measured)."""
+    return round(achieved / read_ceiling, 4) if read_ceiling and read_ceiling > 0 else None
+
+
 def pool_plan(n, stride, free, warmup, steps, cap=0):
     """Batches in the pool (each: n frames at `stride` + n descriptors) and whether a step must re-arm its
     batch inside the timed loop: one fresh batch per step while W + K batches fit in 85 % of the free HBM
@@ -390,8 +396,9 @@ def main():
     ap.add_argument("--alloc", default="slab", choices=("slab", "separate"),
                     help="batch pool as one device allocation (slab, like one UMEM region) or one per batch")
     ap.add_argument("--variant", type=int, default=-1,
-                    help="A/B only: time tuning-library kernel variant N (tools/kbench.py numbering) instead of the "
-                         "shipped entry point; the line is marked and is never the bench value")
+                    help="A/B only: time the product kernel at tuning switch N (tune/xsk_tune_product.hip, "
+                         "xsk_gpu__product_variant) instead of the shipped entry point; the line is marked and is never "
+                         "the bench value")
     ap.add_argument("--opts", type=int, default=0,
                     help="wire-format options (XSK_GPU_OPT_*, xsk_gpu_echo_dev_opts); 0 = the reference's gates")
     args = ap.parse_args()
@@ -446,9 +453,13 @@ def main():
     log(f"[rank {rank}] generated {pool} batches in {time.perf_counter() - t0:.1f} s")
     frame_bytes = int(descss[0].view(torch.int32).view(-1, 4)[:, 2].to(torch.int64).sum().item())
 
-    # one verdict buffer per pooled batch: a re-arm restores batch b from ITS verdicts of its previous use
-    verds = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(pool if rearm_in_loop else 1)]
-    recs = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    # outputs: one verdict and one record buffer per step, so that every step's outputs are checked after the timed
+    # region; when batches are re-armed inside the loop (c5: the pool is smaller than W + K), one verdict
+    # buffer per pooled batch instead -- a re-arm restores batch b from ITS verdicts of its previous use -- and the
+    # records of the last use of each
+    per_step = not rearm_in_loop
+    verds = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(W + K if per_step else pool)]
+    recss = [torch.empty(n * 16, dtype=torch.uint8, device=dev) for _ in range(W + K if per_step else 1)]
     stats = torch.zeros(40, dtype=torch.uint8, device=dev)
     ws = torch.zeros(max(16, X.workspace_size(local, n)), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -458,13 +469,14 @@ def main():
 
     def step(s):
         b = s % pool
-        verd = verds[b % len(verds)]
+        verd = verds[s if per_step else b]
+        recs = recss[s if per_step else 0]
         if rearm_in_loop and s >= pool:
             X.rearm_dev(umems[b], descss[b], verd, n, stream)  # conservative: counted inside the timing
-        if args.variant >= 0:  # A/B timing of a tuning variant (counters as per-workgroup partials in ws)
-            rc = tune.xsk_gpu__echo_variant(args.variant, 0, umems[b].data_ptr(), umems[b].numel(),
-                                            descss[b].data_ptr(), n, verd.data_ptr(), recs.data_ptr(), wsv.data_ptr(),
-                                            stream.cuda_stream)
+        if args.variant >= 0:  # A/B timing of a tuning switch (counters as per-workgroup partials in ws)
+            rc = tune.xsk_gpu__product_variant(args.variant, 0, umems[b].data_ptr(), umems[b].numel(),
+                                               descss[b].data_ptr(), n, verd.data_ptr(), recs.data_ptr(),
+                                               wsv.data_ptr(), stream.cuda_stream)
             assert rc == 0, rc
         else:
             X.echo_dev(umems[b], descss[b], n, verd, recs, stats, ws, stream, opts=args.opts)
@@ -501,12 +513,16 @@ def main():
         kern_ms, launches = ev_ms, K
         timer_src = "HIP events on the launch stream around the K back-to-back launches (one launch per step)"
 
-    # ---- correctness of what was timed: every frame of every step accepted and counted ----
+    # ---- correctness of what was timed: every frame of every step accepted and counted, every step's verdicts
+    # TX_REPLY and records carrying both verified input checksums (checked on the device after the timed region) ----
     st = stats.cpu().numpy().view(X.STATS_DTYPE)[0]
     ok = args.variant >= 0 or (int(st["rx_packets"]) == (W + K) * n and int(st["tx_packets"]) == (W + K) * n)
     ok = ok and all(bool((v == 0).all().item()) for v in verds)
-    recs_np = recs.cpu().numpy().view(X.REC_DTYPE)
-    ok = ok and bool((recs_np["flags"] == 3).all())
+    ok = ok and all(bool((r.view(-1, 16)[:, 1] == 3).all().item()) for r in recss)  # xsk_gpu_rec.flags
+    checked = {"steps_with_outputs_checked": (W + K) if per_step else pool,
+               "verdicts": "every step" if per_step else "the last use of each pooled batch",
+               "records": "every step" if per_step else "the last step",
+               "counters": "every step (rx / tx packets == steps x frames)"}
 
     # read-only streaming ceiling over one batch slab (context for the roofline)
     out = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -552,6 +568,7 @@ def main():
                        "layout": "device-resident UMEM slab + xdp_desc array", "pool_alloc": args.alloc,
                        "rearm_in_timed_region": rearm_in_loop},
             "verified": bool(ok_all == world),
+            "verification": checked,
             **({"ab_variant": args.variant, "note": "A/B timing of a tuning variant, not the shipped kernel"}
                if args.variant >= 0 else {}),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -560,6 +577,9 @@ def main():
                          "kernel": kernel, "kernel_avg_us": round(kern_avg_ms * 1e3, 2), "kernel_timer": timer_src,
                          "algorithmic_bytes_per_launch": frame_bytes,
                          "read_ceiling_gbs": round(read_ceiling, 1),
+                         # the physical bar: a plain 16-B read of the same slab on this GPU (xsk_gpu_stream_read_dev),
+                         # below the 8 TB/s spec, so 0.90 of spec is above what a read can reach
+                         "frac_of_read_ceiling": frac_of_ceiling(achieved, read_ceiling),
                          "note": "rank 0's kernel; every rank's in per_rank"},
             "per_rank": per_rank,
             "event_ms_per_step": round(ev_max / K, 4),

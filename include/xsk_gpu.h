@@ -180,9 +180,10 @@ enum xsk_gpu_mode {
     /* The kernel reads and rewrites the registered host UMEM directly over PCIe (mapped pinned
      * memory): one launch per batch, no copies of frame bytes.  Best for small RX batches. */
     XSK_GPU_MODE_ZEROCOPY = 0,
-    /* The frames' UMEM span is copied host->device, transformed in HBM, and the 64-byte header
-     * window of every frame is copied back (strided 2-D copy when the batch has a uniform
-     * stride).  Best for large batches. */
+    /* The bytes the transform reads are copied host->device (one strided 2-D copy for a uniform stride, one
+     * copy of a densely covered span, else a per-frame gather across PCIe: never more than 1.1 x the bytes the
+     * frames own), transformed in HBM, and only the rewritten header bytes of replies are copied back.  Best
+     * for large batches. */
     XSK_GPU_MODE_STAGED = 1,
     /* ZEROCOPY data path plus a resident polling kernel for the RX loop's small batches: a call with
      * n <= XSK_GPU_LOWLAT_MAX writes the descriptors into mapped host memory, bumps a doorbell the
@@ -199,11 +200,22 @@ enum xsk_gpu_mode {
 /* Resident LOWLAT kernels per device in one process.  Each waits for batches on a highest-priority stream of its
  * own, and the HIP runtime backs a process's streams of one priority with a few hardware queues (GPU_MAX_HW_QUEUES,
  * 4 by default): a resident kernel that lands on a queue behind another one does not start until that one exits,
- * and its batches would time out (tools/rxqueues: 8 LOWLAT queues on one GPU, 4 of them -ETIMEDOUT).  A context
- * created in XSK_GPU_MODE_LOWLAT while XSK_GPU_LOWLAT_PER_DEVICE LOWLAT contexts of this process already exist on
- * its device runs as XSK_GPU_MODE_ZEROCOPY (same results, a launch per batch); xsk_gpu_ctx_mode() reports the mode
- * a context runs in.  xsk_gpu_fini() releases the slot. */
+ * and its batches would time out (tools/rxqueues: 8 LOWLAT queues on one GPU, 4 of them -ETIMEDOUT).  So a device
+ * holds at most min(XSK_GPU_LOWLAT_PER_DEVICE, GPU_MAX_HW_QUEUES) - reserved resident kernels of this process, where
+ * `reserved` is what xsk_gpu_lowlat_reserve() set aside; a context created in XSK_GPU_MODE_LOWLAT beyond that runs as
+ * XSK_GPU_MODE_ZEROCOPY (same results, a launch per batch); xsk_gpu_ctx_mode() reports the mode a context runs in,
+ * and xsk_gpu_fini() releases the slot once its kernel has stopped.
+ * The cap assumes the process runs NO other highest-priority streams on that device: an application stream of the
+ * highest priority (hipStreamCreateWithPriority with the greatest priority, torch.cuda.Stream(priority=-1)) shares
+ * those hardware queues, so its work may wait behind a resident kernel and a resident kernel behind its work.  An
+ * application with such streams reserves one queue per stream first. */
 #define XSK_GPU_LOWLAT_PER_DEVICE 4
+
+/* Reserve `queues` (<= XSK_GPU_LOWLAT_PER_DEVICE) of `device`'s highest-priority hardware queues for the application's
+ * own highest-priority streams: LOWLAT contexts created afterwards stay within the rest (earlier ones keep running).
+ * Process-wide, host-only (no device call).  Returns the resident LOWLAT kernels now allowed on the device, or
+ * -EINVAL. */
+int xsk_gpu_lowlat_reserve(int device, uint32_t queues);
 
 /* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
  * xsk_utils.c:132-135).  The UMEM is page-locked (hipHostRegister) until xsk_gpu_fini().
@@ -216,10 +228,13 @@ int xsk_gpu_ctx_mode(const xsk_gpu_ctx* ctx);
 
 /* Synchronously process one batch of host descriptors against the bound UMEM.  Same outputs as
  * xsk_gpu_echo_dev(); `verdicts`, `recs` and `stats` are host pointers (each may be NULL).
- * XSK_GPU_MODE_LOWLAT: if a doorbell batch is not complete within 2 s the call posts STOP, waits (up to 1 s)
- * for the resident kernel to stop and returns -ETIMEDOUT; the caller then owns that batch's frames again
- * (each may or may not have been transformed).  If the kernel had not stopped by then, every later call
- * returns -EBUSY, touching nothing, until it has (xsk_gpu_fini() waits for it). */
+ * XSK_GPU_MODE_LOWLAT: if a doorbell batch is not complete within 2 s the call posts STOP and waits (up to 1 s)
+ * for the resident kernel to stop.  A workgroup that finds STOP before it took its slice of the batch never serves
+ * it, so once the kernel has stopped every slice is either transformed exactly once or untouched: all served -> the
+ * call returns 0 after all; some served -> the untouched slices take the launch path and the call returns 0; none
+ * served -> -ETIMEDOUT with every frame untouched (a retry transforms them exactly once).  If the kernel had not
+ * stopped within the second, the call returns -ETIMEDOUT with the batch's frames in an unknown state, and every
+ * later call returns -EBUSY, touching nothing, until it has (xsk_gpu_fini() waits for it). */
 int xsk_gpu_process(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                     struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats);
 
@@ -260,8 +275,10 @@ int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, v
  * are independent, xsk_receive.c:113-190), each context runs on its own host thread and stream, and
  * verdicts / records land at the descriptors' own positions.  The four counters are the sum over the
  * contexts (xsk_utils.h:17-23), added to *stats like xsk_gpu_process() does.
- * LOWLAT contexts: the path is chosen per batch -- when a share exceeds XSK_GPU_LOWLAT_MAX every context
- * takes the launch path, so shares of one batch never split between resident kernels and launched grids.
+ * LOWLAT contexts: the path is chosen per batch -- the doorbells only when every context really runs LOWLAT
+ * (xsk_gpu_ctx_mode: requests beyond a device's resident-kernel cap run as ZEROCOPY) and no share exceeds
+ * XSK_GPU_LOWLAT_MAX; otherwise every resident kernel is stopped first and every share is launched, so shares of one
+ * batch never split between resident kernels and launched grids.
  * Partial failure: when any context fails, the call returns the first failing context's error and adds
  * NOTHING to *stats (all or nothing); the shares of the contexts that succeeded are transformed and their
  * verdicts / records written, the failed shares' positions are left as they were -- xsk_gpu_multi_status()

@@ -1,26 +1,32 @@
 /* CPU unit test of the LOWLAT doorbell protocol (xsknet_amd/csrc/xsk_lowlat_proto.h) against a simulated
- * resident grid: normal service over 1..4 workgroups, the leader's idle exit and the Dekker relaunch, an
- * instance that exits without serving, the timeout path (STOP posted, the instance waited for, -ETIMEDOUT),
- * the broken channel (-EBUSY until the instance has stopped, then recovery), the slice and group choices.
- * Built and run by tests/test_lowlat_proto.py. */
+ * resident grid that follows the kernel's order (xsk_lowlat.hip, poll_doorbell/examine): a workgroup that sees a new
+ * batch with STOP in the same command word retires it unserved (cancel = done = seq) instead of serving it.
+ * Cases: normal service over 1..4 workgroups, the leader's idle exit and the Dekker relaunch, an instance that exits
+ * without serving, the timeout with nothing served (an instance still queued when the call gave up -- ADVICE r03),
+ * with part of the batch served, with the batch finished by an instance that was inside its body (a late
+ * completion: 0), the broken channel (-EBUSY until the instance has stopped, then recovery), and in every case that
+ * no relaunched grid ever serves a batch whose call has returned.  Built and run by tests/test_lowlat_proto.py. */
 #include <assert.h>
 #include <stdio.h>
 #include <string.h>
 
 #include "../../xsknet_amd/csrc/xsk_lowlat_proto.h"
 
-/* The simulated device: `running` instances of the grid (the stream), served[g] = the last seq workgroup g
- * completed.  Time advances by one tick per relax / now call. */
+/* The simulated device: `running` instances of the grid (the stream); served[g] = each workgroup's baseline (taken
+ * from `done` at launch, as the kernel does).  Time advances by one tick per relax / now call. */
 struct sim {
     struct xsk_gpu__bell bell;
     double t;
-    int running;     /* instances running or queued */
+    int running;              /* instances running or queued */
     int launches;
-    int serve_after; /* relax steps before a running instance serves a posted batch (-1: never) */
-    int stop_after;  /* relax steps a STOP takes to drain the stream (-1: never) */
+    int serve_after;          /* relax steps before a running instance serves a posted batch (-1: never) */
+    uint32_t serve_mask;      /* workgroups that serve before a STOP (bit g) */
+    int mid_body;             /* on STOP, the serving workgroups are inside the body: they finish it (done, no cancel) */
+    int stop_after;           /* relax steps a STOP takes to drain the stream (-1: never) */
     int exit_without_serving; /* the next instance exits at once, serving nothing */
     int countdown, stop_countdown;
-    int leader_gone;  /* the leader has cleared alive (idle exit) */
+    uint32_t served[XSK_GPU__LL_WG];
+    int serves;               /* slices transformed, over the whole test */
 };
 
 static int sim_launch(void* u) {
@@ -28,8 +34,8 @@ static int sim_launch(void* u) {
     s->launches++;
     s->running++;
     s->countdown = s->serve_after;
+    for (uint32_t g = 0; g < XSK_GPU__LL_WG; g++) s->served[g] = s->bell.wg[g].done; /* the kernel's baseline */
     __atomic_store_n(&s->bell.wg[0].alive, 1u, __ATOMIC_SEQ_CST);
-    s->leader_gone = 0;
     return 0;
 }
 static int sim_idle(void* u) { return ((struct sim*)u)->running == 0; }
@@ -38,23 +44,38 @@ static void sim_relax(void* u) {
     struct sim* s = (struct sim*)u;
     s->t += 1e-6;
     if (!s->running) return;
-    const uint64_t c = s->bell.cmd;
-    if (c & XSK_GPU__BELL_STOP) {
-        if (s->stop_countdown < 0) s->stop_countdown = 0;
-    }
     if (s->exit_without_serving) {
         s->exit_without_serving = 0;
         s->running = 0;
         s->bell.wg[0].alive = 0;
         return;
     }
+    const uint64_t c = s->bell.cmd;
+    const uint32_t seq = (uint32_t)c;
+    const int stop = (c & XSK_GPU__BELL_STOP) != 0;
     uint32_t w = (uint32_t)(c >> 56) & 7u;
     w = w ? w : 1u;
-    if (s->serve_after >= 0 && (uint32_t)s->bell.wg[0].done != (uint32_t)c && !(c & XSK_GPU__BELL_STOP)) {
-        if (s->countdown-- <= 0)
-            for (uint32_t g = 0; g < w; g++) s->bell.wg[g].done = (uint32_t)c;
+    const int due = s->serve_after >= 0 && s->countdown-- <= 0;
+    for (uint32_t g = 0; g < XSK_GPU__LL_WG; g++) {
+        if (s->served[g] == seq) continue;
+        if (g >= w) { /* not serving this batch */
+            s->served[g] = seq;
+            continue;
+        }
+        if (stop && !s->mid_body) { /* the kernel's order: STOP before taking a batch -> retire it unserved */
+            s->bell.wg[g].cancel = seq;
+            s->bell.wg[g].done = seq;
+            s->served[g] = seq;
+            continue;
+        }
+        if ((stop && s->mid_body) || (due && ((s->serve_mask >> g) & 1u))) {
+            s->bell.wg[g].done = seq;
+            s->served[g] = seq;
+            s->serves++;
+        }
     }
-    if (c & XSK_GPU__BELL_STOP) {
+    if (stop) {
+        if (s->stop_countdown < 0) s->stop_countdown = 0;
         if (s->stop_after >= 0 && s->stop_countdown++ >= s->stop_after) {
             s->running = 0;
             s->bell.wg[0].alive = 0;
@@ -72,6 +93,7 @@ int main(void) {
     struct sim S;
     memset(&S, 0, sizeof S);
     S.stop_countdown = -1;
+    S.serve_mask = 0xFu;
     struct xsk_gpu__ll_state st;
     memset(&st, 0, sizeof st);
     st.bell = &S.bell;
@@ -79,69 +101,104 @@ int main(void) {
     st.quiesce_s = 0.005;
     st.recheck_s = 1e-4;
     struct xsk_gpu__ll_ops o = ops_of(&S);
+    uint32_t un = 0xFFu;
 
     /* 1. normal service: the first call launches, later calls reuse the running grid */
     S.serve_after = 5;
     S.stop_after = 3;
     for (uint32_t w = 1; w <= XSK_GPU__LL_WG; w++) {
-        assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64 * w), w) == 0);
+        assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64 * w), w, &un) == 0 && un == 0);
         for (uint32_t g = 0; g < w; g++) assert(S.bell.wg[g].done == st.seq);
     }
     assert(S.launches == 1 && st.seq == XSK_GPU__LL_WG && st.launched);
+    assert(S.serves == 1 + 2 + 3 + 4);
 
     /* 2. the leader left (idle exit) before the post: relaunch, stream-ordered behind the old instance */
     S.bell.wg[0].alive = 0;
-    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(10), 1) == 0);
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(10), 1, &un) == 0);
     assert(S.launches == 2);
 
     /* 3. an instance that exits without serving the batch: the periodic check relaunches it */
     S.running = 0;
     S.bell.wg[0].alive = 1; /* looked alive at the post */
     int before = S.launches;
-    S.serve_after = -1; /* the current (non-existent) instance never serves ... */
-    S.running = 0;
-    {
-        /* ... so the recheck must find the stream idle and launch; the new instance then serves */
-        struct xsk_gpu__ll_ops o2 = o;
-        S.serve_after = 3;
-        S.exit_without_serving = 0;
-        st.launched = 1;
-        assert(xsk_gpu__ll_run(&st, &o2, XSK_GPU__BELL_N(7), 1) == 0);
-    }
+    S.serve_after = 3;
+    st.launched = 1;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(7), 1, &un) == 0);
     assert(S.launches == before + 1);
 
-    /* 4. timeout, the instance stops on STOP: -ETIMEDOUT, not broken, nothing running */
+    /* 4. timeout with nothing served -- the instance was still queued (it never took the batch before the call gave
+     *    up): it sees STOP with the batch and retires it unserved, so the call reports every slice
+     *    untouched, the channel is not broken, and no relaunch serves that batch */
     S.serve_after = -1;
     S.stop_after = 10;
     S.stop_countdown = -1;
-    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1) == -ETIMEDOUT);
-    assert(!st.broken && !st.launched && S.running == 0);
-    assert(S.bell.cmd & XSK_GPU__BELL_STOP);
-    /* the next call launches afresh and is served */
+    int serves = S.serves;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1, &un) == -ETIMEDOUT);
+    assert(un == 1u && !st.broken && !st.launched && S.running == 0);
+    assert((S.bell.cmd & XSK_GPU__BELL_STOP) && (uint32_t)S.bell.cmd == st.seq && ((S.bell.cmd >> 32) & 0xFFFFu) == 64);
+    assert(S.bell.wg[0].cancel == st.seq && S.bell.wg[0].done == st.seq && S.serves == serves);
+    /* the next call launches afresh (the launch re-posts the cancelled command without STOP: the new grid's baseline
+     * is the retired seq, so only the new batch is served) */
     S.serve_after = 2;
-    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1) == 0 && S.bell.wg[0].done == st.seq);
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1, &un) == 0 && S.bell.wg[0].done == st.seq);
+    assert(S.serves == serves + 1);
 
-    /* 5. timeout, the instance does NOT stop within quiesce_s: broken; -EBUSY (nothing posted) until it does */
+    /* 4b. the same on four workgroups, with workgroups 1-3 never having seen any batch (their `done` lags) */
+    S.serve_after = -1;
+    S.stop_after = 4;
+    S.stop_countdown = -1;
+    serves = S.serves;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(1024), 4, &un) == -ETIMEDOUT && un == 0xFu && !st.broken);
+    for (uint32_t g = 0; g < 4; g++) assert(S.bell.wg[g].done == st.seq);
+    S.serve_after = 1;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(1024), 4, &un) == 0 && un == 0 && S.serves == serves + 4);
+
+    /* 5. timeout with part of the batch served: the leader served its slice, workgroup 1 never took its own before
+     *    STOP -> -ETIMEDOUT, slice 1 untouched (the library finishes it through the launch path) */
+    S.serve_after = 1;
+    S.serve_mask = 0x1u;
+    S.stop_after = 3;
+    S.stop_countdown = -1;
+    serves = S.serves;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(512), 2, &un) == -ETIMEDOUT);
+    assert(un == 0x2u && !st.broken && S.serves == serves + 1);
+    assert(S.bell.wg[1].cancel == st.seq && S.bell.wg[0].cancel != st.seq);
+    S.serve_mask = 0xFu;
+
+    /* 6. late completion: the serving workgroups were inside the body when STOP arrived; they finish (done, no
+     *    cancel) and the call returns 0 -- every slice served exactly once */
+    S.serve_after = -1;
+    S.mid_body = 1;
+    S.stop_after = 2;
+    S.stop_countdown = -1;
+    serves = S.serves;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(300), 3, &un) == 0 && un == 0 && S.serves == serves + 3);
+    S.mid_body = 0;
+
+    /* 7. timeout, the instance does NOT stop within quiesce_s: broken (outcome unknown: every bit); -EBUSY (nothing
+     *    posted) until it does; then the stopped instance's batch is retired and never served by the relaunch */
     S.serve_after = -1;
     S.stop_after = -1;
     S.stop_countdown = -1;
-    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1) == -ETIMEDOUT);
-    assert(st.broken && S.running > 0);
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1, &un) == -ETIMEDOUT);
+    assert(st.broken && S.running > 0 && un == 1u);
     const uint32_t seq_broken = st.seq;
     const uint64_t cmd_broken = S.bell.cmd;
-    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1) == -EBUSY);
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1, &un) == -EBUSY);
     assert(st.seq == seq_broken && S.bell.cmd == cmd_broken); /* nothing posted */
-    S.running = 0; /* the instance finally stopped */
+    S.running = 0; /* the instance finally stopped (without reaching the batch) */
     S.serve_after = 1;
     S.stop_after = 3;
-    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1) == 0);
-    assert(!st.broken && st.seq == seq_broken + 1 && S.bell.wg[0].done == st.seq);
+    serves = S.serves;
+    assert(xsk_gpu__ll_run(&st, &o, XSK_GPU__BELL_N(64), 1, &un) == 0);
+    assert(!st.broken && st.seq == seq_broken + 1 && S.bell.wg[0].done == st.seq && S.serves == serves + 1);
 
-    /* 6. stop: drains and clears */
+    /* 8. stop: drains and clears */
     assert(xsk_gpu__ll_stop(&st, &o, -1.0) == 0 && !st.launched && S.running == 0);
     assert(xsk_gpu__ll_stop(&st, &o, -1.0) == 0); /* idempotent */
 
-    /* 7. slices: contiguous, multiples of 4 (but the last), covering [0, n) exactly */
+    /* 9. slices: contiguous, multiples of 4 (but the last), covering [0, n) exactly */
     for (uint32_t n = 1; n <= XSK_GPU_LOWLAT_MAX; n++)
         for (uint32_t w = 1; w <= XSK_GPU__LL_WG; w++) {
             uint32_t next = 0;
@@ -155,7 +212,7 @@ int main(void) {
             assert(next == n);
         }
 
-    /* 8. groups: <= 64 frames on the leader; 1024 x 1500 B on every workgroup; 300 x 64 B on 2 */
+    /* 10. groups: <= 64 frames on the leader; 1024 x 1500 B on every workgroup; 300 x 64 B on 2 */
     struct xsk_gpu_desc d[XSK_GPU_LOWLAT_MAX];
     for (int i = 0; i < (int)XSK_GPU_LOWLAT_MAX; i++) {
         d[i].addr = 4096u * i;

@@ -158,6 +158,21 @@ def test_traffic_provenance(tmp_path):
     assert bench.traffic_from_profiles("c3", k, "abc", str(tmp_path / "none.json"))[0] is None
 
 
+def test_frac_of_read_ceiling_on_a_fake_line():
+    """roofline.frac_of_read_ceiling = achieved / read_ceiling_gbs: on round 3's driver line (c3, 5 655 GB/s
+    of frame bytes per kernel time, the read ceiling 6 960 GB/s measured beside it) it is 0.8125, against 0.707 of the
+    8 TB/s spec; no ceiling -> None."""
+    bench = _bench()
+    line = {"roofline": {"achieved": 5655.0, "peak": bench.HBM_PEAK_GBS, "read_ceiling_gbs": 6960.0}}
+    r = line["roofline"]
+    r["frac_of_read_ceiling"] = bench.frac_of_ceiling(r["achieved"], r["read_ceiling_gbs"])
+    assert r["frac_of_read_ceiling"] == 0.8125
+    assert r["frac_of_read_ceiling"] > r["achieved"] / r["peak"]
+    assert bench.frac_of_ceiling(5655.0, 0.0) is None and bench.frac_of_ceiling(5655.0, None) is None
+    # the 0.90-of-spec target sits above the ceiling itself: 0.90 x 8000 > 6960
+    assert 0.90 * bench.HBM_PEAK_GBS > r["read_ceiling_gbs"]
+
+
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_c5_pool_plan(world):
     """c5 splits 64 M x 1500-B frames (2 KiB stride) over the ranks: the per-rank batch, the pool that fits a

@@ -5,10 +5,10 @@ separate `bench.py --variant` runs.  This tool times several variants inside ONE
 never-touched batches: in round r, batch b runs variant V[(b + r) % len(V)], so every variant sees every
 pool position; each launch is bracketed by its own pair of HIP events on the launch stream.  Between rounds
 the pool is regenerated (untimed), so diagnostic variants with wrong results cannot poison the next round.
-Variant -1 is the shipped entry point (xsk_gpu_echo_dev); 1000 + v is the product kernel's source at the
-alternative switch v of tune/xsk_tune_product.hip (xsk_gpu__product_variant).
+Variant -1 is the shipped entry point (xsk_gpu_echo_dev); v >= 0 is the product kernel's source at the alternative
+switch v of tune/xsk_tune_product.hip (xsk_gpu__product_variant; 1000 + v is accepted too, the round-3 numbering).
 
-    python tools/abbench.py --config c3 --variants=-1,131,139 --rounds 3
+    python tools/abbench.py --config c4 --variants=-1,9 --rounds 8
 """
 import argparse
 import json
@@ -27,7 +27,7 @@ import xsknet_amd as X  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--variants", default="-1,131")
+    ap.add_argument("--variants", default="-1,0")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--pool", type=int, default=0, help="batches in the pool (0: as many as fit, <= 24)")
     ap.add_argument("--burst", type=int, default=0,
@@ -59,17 +59,9 @@ def main():
         u = slab[b * bb:(b + 1) * bb]
         if v < 0:
             X.echo_dev(u, descs[b], n, verd, recs, stats, ws, stream)
-        elif v >= 2000:  # the SLACK candidate (tune/xsk_tune_slack.hip)
-            rc = tune.xsk_gpu__slack_variant(v - 2000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
-                                             verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
-            assert rc == 0, rc
-        elif v >= 1000:
-            rc = tune.xsk_gpu__product_variant(v - 1000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
-                                               verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
-            assert rc == 0, rc
         else:
-            rc = tune.xsk_gpu__echo_variant(v, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n, verd.data_ptr(),
-                                            recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
+            rc = tune.xsk_gpu__product_variant(v % 1000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
+                                               verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
             assert rc == 0, rc
 
     # warm-up: every variant once on a batch that is then regenerated

@@ -1,6 +1,6 @@
-# Round-3 full pass, part 1 (run through gpurun): PMC FETCH_SIZE / WRITE_SIZE / SQ passes of the c3, c4 and c2 benches
+# Full pass, part 1 (run through gpurun): PMC FETCH_SIZE / WRITE_SIZE / SQ passes of the c3, c4 and c2 benches
 # and their summaries (they carry the build id; copy gpurun_out/<tag>/traffic_*.json to profiles/ afterwards, so
-# part 2's bench lines attach them).   Usage: bash tools/gpu_full_r03a.sh <tag>
+# part 2's bench lines attach them).   Usage: bash tools/gpu_full_a.sh <tag>
 cd "$GRAFT_REPO_ROOT" || exit 3
 O=gpurun_out/${1:-fulla}
 mkdir -p $O

@@ -1,5 +1,5 @@
-# Round-3 full pass, part 2: the GPU suite, smoke, the bench lines (with part 1's traffic summaries in profiles/), the
-# N = 2 shared-GPU rehearsal and the rocprofv3 kernel-trace summary of every config.   Usage: bash tools/gpu_full_r03b.sh <tag>
+# Full pass, part 2: the GPU suite, smoke, the bench lines (with part 1's traffic summaries in profiles/), the
+# N = 2 shared-GPU rehearsal and the rocprofv3 kernel-trace summary of every config.   Usage: bash tools/gpu_full_b.sh <tag>
 cd "$GRAFT_REPO_ROOT" || exit 3
 O=gpurun_out/${1:-fullb}
 mkdir -p $O

@@ -7,7 +7,10 @@ in batches of 64 (RX_BATCH_SIZE, xsk_utils.h:8) up to 4096 frames, for the zeroc
 UMEM (untimed) so every call transforms echo requests.  Prints one JSON line per (frame length, mode, batch).
 
   python tools/hostlat.py [--lens 64,1500] [--modes zerocopy,staged,lowlat] [--batches 64,256,1024,4096]
-                          [--gpus 0,0] [--reps 200]
+                          [--gpus 0,0] [--reps 200] [--scramble]
+
+--scramble puts the descriptors in a random order over the UMEM's chunks: the RX ring of a client after its free stack
+(xsk_receive.c:55-71) has recycled frames in arbitrary order, so a batch's frames scatter over the 16 MiB.
 """
 import argparse
 import itertools
@@ -40,7 +43,7 @@ def run_one(exe, p, flen, mode, batch, tile, args):
     kv = dict(x.split("=") for x in r.stdout.split())
     us = float(kv["us_per_call"])
     rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto", "groups": args.groups or "auto",
-           "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge),
+           "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge), "scrambled": bool(args.scramble),
            "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3), "calls": int(kv["calls"])}
     if "trace_ns" in kv:  # LOWLAT: the last batch's phases on the GPU
         t = [int(x) for x in kv["trace_ns"].split(",")]
@@ -66,6 +69,7 @@ def main():
     ap.add_argument("--huge", action="store_true", help="the UMEM on transparent huge pages (2 MiB)")
     ap.add_argument("--tiles", default="", help="LOWLAT frames per wave to sweep (echo_replay tile=), e.g. 4,16,64")
     ap.add_argument("--groups", type=int, default=0, help="LOWLAT serving workgroups (echo_replay groups=; 0: by size)")
+    ap.add_argument("--scramble", action="store_true", help="descriptors in a random order over the UMEM's chunks")
     args = ap.parse_args()
     exe = os.path.join(ROOT, "tools", "echo_replay")
     n, chunk = 4096, 4096
@@ -74,6 +78,8 @@ def main():
         for flen in (int(x) for x in args.lens.split(",")):
             umem = np.zeros(n * chunk, np.uint8)
             descs = oracle.synth_batch(umem, n, 256, chunk, seed=0x5EED0001, mode=0, len_lo=flen, len_hi=flen)
+            if args.scramble:
+                descs = np.ascontiguousarray(descs[np.random.default_rng(0x5C).permutation(n)])
             umem.tofile(p("u"))
             descs.tofile(p("d"))
             for mode, batch in itertools.product(args.modes.split(","), (int(x) for x in args.batches.split(","))):

@@ -22,7 +22,7 @@ __all__ = [
     "LIB_PATH", "lib", "build_id", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
-    "MODE_ZEROCOPY", "MODE_STAGED", "MODE_LOWLAT", "LOWLAT_MAX", "MultiContext", "tune_lib", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
+    "MODE_ZEROCOPY", "MODE_STAGED", "MODE_LOWLAT", "LOWLAT_MAX", "MultiContext", "tune_lib", "lowlat_reserve", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
     "classify_dev", "XDP_DROP", "XDP_PASS", "XDP_REDIRECT", "DROP_BAD_IP", "DROP_BAD_CSUM",
     "OPT_STRICT_IPV4", "OPT_VLAN", "OPT_VERIFY_CSUM", "OPT_ALL", "F_IP_CSUM_OK", "F_ICMP_CSUM_OK", "F_VLAN",
     "F_IP_OPTIONS",
@@ -30,7 +30,8 @@ __all__ = [
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libxsknet_amd.so")
-# kernel variants for the tuning sweep (tools/kbench.py) and their parity tests; never the product path
+# the product kernel at alternative switch values for in-process A/B (tools/abbench.py) and its parity tests; never
+# the product path
 TUNE_LIB_PATH = os.path.join(_HERE, "libxsknet_amd_tune.so")
 
 TX_REPLY, DROP_SHORT, DROP_NOT_IPV4, DROP_NOT_ICMP, DROP_NOT_ECHO, DROP_BAD_DESC, DROP_BAD_IP, DROP_BAD_CSUM = range(8)
@@ -121,14 +122,13 @@ _SIGS = {
     "xsk_gpu__multi_inject": ([_P, C.c_uint32, C.c_int], C.c_int),
     "xsk_gpu__lowlat_tune": ([_P, C.c_uint32, C.c_uint32, C.c_uint32], C.c_int),
     "xsk_gpu_multi_fini": ([_P], None),
+    "xsk_gpu_lowlat_reserve": ([C.c_int, C.c_uint32], C.c_int),
+    "xsk_gpu__staged_stats": ([_P, C.POINTER(C.c_uint64)], C.c_int),
     # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
     "xsk_gpu__echo_dev_grid": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32], C.c_int),
 }
 _TUNE_SIGS = {
-    "xsk_gpu__echo_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
-    "xsk_gpu__echo_wire_variant": ([C.c_int, _P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P], C.c_int),
     "xsk_gpu__product_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
-    "xsk_gpu__slack_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
 }
 _tune: Optional[C.CDLL] = None
 
@@ -149,7 +149,7 @@ def lib() -> C.CDLL:
 
 
 def tune_lib() -> C.CDLL:
-    """libxsknet_amd_tune.so: the kernel variants of the tuning sweep (tests and tools/ only)."""
+    """libxsknet_amd_tune.so: the product kernel at alternative switch values (tools/abbench.py, tests only)."""
     global _tune
     if _tune is None:
         lib()
@@ -243,6 +243,15 @@ def stream_read_dev(src, nbytes: int, out, stream=None) -> None:
                                                                     _stream_ptr(stream)))
 
 
+def lowlat_reserve(device: int, queues: int) -> int:
+    """xsk_gpu_lowlat_reserve: set aside highest-priority hardware queues of `device` for the application's own
+    highest-priority streams; returns the resident LOWLAT kernels now allowed there."""
+    rc = lib().xsk_gpu_lowlat_reserve(device, queues)
+    if rc < 0:
+        raise XskGpuError("xsk_gpu_lowlat_reserve", rc)
+    return rc
+
+
 def timing_enable(on: bool = True) -> None:
     _check("xsk_gpu_timing_enable", lib().xsk_gpu_timing_enable(1 if on else 0))
 
@@ -286,6 +295,13 @@ class EchoContext:
             self._ctx, descs.ctypes.data, n, verdicts.ctypes.data, recs.ctypes.data if recs is not None else None,
             stats.ctypes.data))
         return verdicts, recs, stats[0]
+
+    def staged_stats(self):
+        """xsk_gpu__staged_stats of a STAGED context: bytes copied host->device since init, and the chunks copied as
+        one 2-D stride / one dense span / by the gather kernel."""
+        out = (C.c_uint64 * 4)()
+        _check("xsk_gpu__staged_stats", lib().xsk_gpu__staged_stats(self._ctx, out))
+        return {"h2d_bytes": out[0], "strided": out[1], "span": out[2], "gather": out[3]}
 
     def lowlat_tune(self, tile_frames: int = 0, groups: int = 0, timeout_us: int = 0) -> None:
         """Tool / test knobs of a LOWLAT context (xsk_gpu__lowlat_tune): frames per wave, serving workgroups,

@@ -2,6 +2,10 @@
 // compiles) at alternative values of its remaining template switches, for in-process A/B against the shipped
 // instance (tools/abbench.py variants >= 1000, bench.py --variant).  Tuning library only.
 //   0  as shipped (reference mode)            2  wire mode as shipped (every option)
+// (round 4 removed the round-1/2 laboratory -- tune/xsk_echo_lab.h, xsk_echo_variants.h, xsk_tune.hip, xsk_wire_v1.hip,
+// the variants of tools/kbench.py and bench.py --variant < 1000 -- and the SLACK patch unit: every variant there lost
+// by more than 2 % in a committed A/B log or was shipped; the logs under profiles/r01-r03 and DESIGN.md stay the record,
+// and the sources are in git history before commit "Prune the tuning laboratory".)
 // (round 3 also measured RMETA -- ranked streams reading their step's metadata rows in rank order, one LDS read
 // per step instead of two dependent ones: c4 195.5 vs 187.2 us, profiles/r03/ab_rank_ordered_meta_*.log -- and
 // ROLL, the tiles of a round in a rolled loop so the kernel's code shrinks from 78 to 46 KB: c4 185.9 vs 185.9 us,
@@ -47,12 +51,12 @@ __global__ __launch_bounds__(kThreads6, 1) void timed_round_kernel(EchoArgs a, u
         for (uint32_t k = 0;; ++k) {
             const uint32_t tb = (k * gridDim.x + blockIdx.x) * kRound;
             if (tb >= ntiles) break;
-            echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy>(a, tb, min(ntiles, tb + kRound), sm);
+            echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack>(a, tb, min(ntiles, tb + kRound), sm);
         }
     } else {
         const uint32_t g = (PERM == 1 && (blockIdx.x ^ 1u) < gridDim.x) ? blockIdx.x ^ 1u : blockIdx.x;
         const uint32_t t_begin = g * per, t_end = min(ntiles, t_begin + per);
-        echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy>(a, t_begin, t_end, sm);
+        echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack>(a, t_begin, t_end, sm);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -98,6 +102,9 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         // 7 / 8: without PRIO (a stream batch's address work and loads at the default priority), reference / wire mode
         case 7: echo_round_kernel<false, false, kUR, true, false><<<gg, bb, 0, s>>>(args, per); break;
         case 8: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, false><<<gg, bb, 0, s>>>(args, per); break;
+        // 9: SLACK 0 -- heavy waves wait for every wave of the workgroup (round 3's write-phase wait); 13: SLACK 4
+        case 9: echo_round_kernel<false, false, kUR, true, true, 0><<<gg, bb, 0, s>>>(args, per); break;
+        case 13: echo_round_kernel<false, false, kUR, true, true, 4><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
@@ -106,4 +113,9 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
     }
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+// The tuning library's own copy of the error hook (the product library's is hidden).
+extern "C" __attribute__((visibility("hidden"))) int xsk_gpu__hip_fail(hipError_t e) {
+    return e == hipErrorOutOfMemory ? -ENOMEM : -EIO;
 }

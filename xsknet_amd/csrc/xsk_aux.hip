@@ -1,10 +1,11 @@
 // xsk_aux.hip — bench / test utilities of the C ABI (not on the hot path): the synthetic frame
-// generator (bit-identical to oracle/echo_oracle.c), re-arm, the staged-mode header gather and the
-// read-only streaming ceiling.
+// generator (bit-identical to oracle/echo_oracle.c), re-arm, the staged-mode copy-in gather and header gather, and
+// the read-only streaming ceiling.
 #include <errno.h>
 
 #include "../../include/xsk_gpu.h"
 #include "xsk_echo_kernels.h"
+#include "xsk_gpu_internal.h"
 #include "xsk_hip_util.h"
 
 using namespace xskgpu;
@@ -130,6 +131,35 @@ __global__ __launch_bounds__(256) void pack_headers_kernel(const uint8_t* umem, 
     uint8_t* q = pack + (uint64_t)i * kPack;
     const uint32_t w = wire ? min(descs[i].len, kPack) : 38u;
     for (uint32_t k = 0; k < w; ++k) q[k] = p[k];
+}
+
+// Staged host mode, scattered descriptors: copy every frame's read span from the mapped host UMEM (across PCIe) into
+// the device mirror at the same offset.  One 16-lane row per frame (4 frames per wave), 256-B row-loads, four in
+// flight per lane before the stores -- a batch's PCIe reads overlap like the zerocopy kernel's.  Only the bytes the
+// transform will read move (xsk_gpu__read_span), never the gaps between frames.
+__global__ __launch_bounds__(256) void stage_gather_kernel(const uint8_t* src, uint8_t* dst, uint64_t umem_size,
+                                                           const xsk_gpu_desc* descs, uint32_t n, uint32_t wire) {
+    const uint32_t f = (blockIdx.x * 256u + threadIdx.x) >> 4, k = threadIdx.x & 15u;
+    if (f >= n) return;
+    const xsk_gpu_desc d = descs[f];
+    uint64_t a16 = 0;
+    const uint64_t span = xsk_gpu__read_span(d.addr, d.len, umem_size, (int)wire, &a16);
+    const u32x4* s = (const u32x4*)(src + a16);
+    u32x4* t = (u32x4*)(dst + a16);
+    const uint64_t nv = span >> 4;  // 16-B vectors
+    for (uint64_t v0 = 0; v0 < nv; v0 += 64u) {
+        u32x4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t v = v0 + 16u * (uint32_t)u + k;
+            if (v < nv) x[u] = __builtin_nontemporal_load(s + v);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t v = v0 + 16u * (uint32_t)u + k;
+            if (v < nv) t[v] = x[u];
+        }
+    }
 }
 
 // csum_replace2(csum, 0, 8) on the LE-loaded field: the inverse of the transform's (8 -> 0) patch
@@ -272,6 +302,21 @@ int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_d
     hipLaunchKernelGGL(pack_headers_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t*)d_umem, d_descs, d_verdicts, n, d_pack, wire);
     HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int xsk_gpu__stage_gather_dev(const void* m_umem, void* d_mirror, uint64_t umem_size, const struct xsk_gpu_desc* d_descs,
+                              uint32_t n, uint32_t wire, void* stream) {
+    if (n == 0) return 0;
+    if (n > XSK_GPU_MAX_BATCH || !m_umem || !d_mirror || !d_descs) return -EINVAL;
+    // <= 2^24 frames (2^22 workgroups) per launch
+    constexpr uint32_t kChunk = 1u << 24;
+    for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+        const uint32_t m = n - c0 < kChunk ? n - c0 : kChunk;
+        hipLaunchKernelGGL(stage_gather_kernel, dim3((m + 15u) / 16u), dim3(256), 0, (hipStream_t)stream,
+                           (const uint8_t*)m_umem, (uint8_t*)d_mirror, umem_size, d_descs + c0, m, wire);
+        HIP_TRY(hipGetLastError());
+    }
     return 0;
 }
 

@@ -28,6 +28,9 @@ constexpr int kUR = 6;                      // the same for the launched kernel'
 constexpr int kRefTPW = 2;                  // reference mode: tiles per wave per round (2048 frames per CU)
 constexpr int kRefHeavy = 512;              // reference mode: SYNC 2's heavy-frame threshold (bytes)
 constexpr int kWireHeavy = 1024;            // wire mode: the same
+constexpr int kRefSlack = 2;                // reference mode: a heavy wave writes once all but 2 waves have read the
+                                            // round (SLACK): c4 181.4 -> 176.5 us, c3 274.0 -> 272.9 in-process A/B
+                                            // (profiles/r03/ab_slack_confirm_*.log)
 
 struct EchoArgs {
     uint8_t* umem;
@@ -849,8 +852,8 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // low-latency resident kernel (xsk_lowlat.hip) once per doorbell.
 //   TPW   tiles per wave per round (reference mode 2; wire mode, whose windows are 128 B, and sub-tiles 1)
 //   SYNC  how a wave enters its write phase.  0: at once (one-round small batches); 2: a wave at least half
-//         of whose frames this round have >= HEAVY bytes waits until every wave of the workgroup has read the
-//         round (LDS arrival counter), lighter waves go ahead -- the phase separation pays where reads
+//         of whose frames this round have >= HEAVY bytes waits until every wave of the workgroup but SLACK has
+//         read the round (LDS arrival counter), lighter waves go ahead -- the phase separation pays where reads
 //         dominate, and costs latency hiding where frames are short
 //   WIRE  the wire-format mode (a.opts != 0): 128-B windows, wire_header_phase
 //   SUBT  tiles of a.tile_live frames (small batches: the batch spreads over every wave)
@@ -863,11 +866,12 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
     static_assert(SYNC == 0 || SYNC == 2, "write phases: at once (0) or heavy waves wait for the round (2)");
+    static_assert(SLACK >= 0 && SLACK < kWaves6, "SLACK: waves a heavy wave does not wait for");
     constexpr int U = kU;
     constexpr bool REF = !WIRE;                          // reference-mode stream choices (D2 / MID / SKM)
     constexpr bool PAIR = REF && TPW == 2 && !SUBT;      // paired short tiles
@@ -1103,8 +1107,9 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             ++rounds_done;
             if (lane == 0) atomicAdd(&s_arrive, 1u);
             if (uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
+                // (every wave but SLACK: the last waves of a round are usually ragged ones still streaming)
                 while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                       rounds_done * (uint32_t)kWaves6)
+                       rounds_done * (uint32_t)kWaves6 - (uint32_t)SLACK)
                     __builtin_amdgcn_s_sleep(2);
             }
         }
@@ -1159,7 +1164,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
-template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT>
+template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
+          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1167,7 +1173,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
+               SLACK>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.

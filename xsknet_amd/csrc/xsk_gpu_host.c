@@ -13,13 +13,15 @@
  *             launch (two when it spans more than one workgroup) and one synchronisation, no copies.
  *   LOWLAT:   ZEROCOPY, but batches of <= XSK_GPU_LOWLAT_MAX frames go to a resident polling kernel
  *             through a doorbell in mapped host memory (xsk_lowlat.hip): no launch, no synchronisation.
- *   STAGED:   frames are copied host->device into a device mirror of the UMEM (one strided 2-D copy
- *             when the chunk has a uniform frame stride, else the chunk's byte span), transformed in
- *             HBM, and only the 38 rewritten header bytes of TX_REPLY frames are copied back and
- *             scattered into the UMEM — bytes the batch does not own are never written.  Batches of
- *             more than one chunk run as a two-stream pipeline: the copy-in of chunk i+1 overlaps the
- *             kernel and the copy-back of chunk i, and the host scatters chunk i while later chunks
- *             are still in flight.
+ *   STAGED:   the bytes the transform reads are copied host->device into a device mirror of the UMEM (one
+ *             strided 2-D DMA copy when the chunk has a uniform frame stride, one copy of the chunk's span when its
+ *             frames cover it densely, else -- AF_XDP's recycled, scattered descriptors -- a gather kernel that
+ *             moves each frame's own bytes across PCIe), transformed in HBM, and only the 38 rewritten header
+ *             bytes of TX_REPLY frames are copied back and scattered into the UMEM — bytes the batch does not own
+ *             are never written.  Batches of more than one chunk run as a two-stream pipeline: chunk i+1's
+ *             copy-in waits for chunk i's header pack (a frame's read span may reach into a neighbour's first
+ *             bytes, which chunk i may just have rewritten in the mirror), its copy-back overlaps chunk i+1's
+ *             copy-in, and the host scatters chunk i while later chunks are still in flight.
  */
 #define _GNU_SOURCE
 #define __HIP_PLATFORM_AMD__ 1
@@ -58,24 +60,59 @@ struct xsk_gpu_ctx {
     struct xsk_gpu_desc* m_descs;  /* ZEROCOPY: device aliases of h_descs / h_verd / h_stats */
     uint8_t* m_verd;
     struct xsk_gpu_stats* m_stats;
+    uint8_t* m_umem;  /* STAGED: the mapped alias of umem (the gather kernel's source) */
     hipStream_t stream[NSTREAMS];
     hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
+    hipEvent_t* packed; /* STAGED [max_chunks]: chunk's rewritten headers are packed (its mirror bytes are free) */
+    uint64_t staged[4]; /* STAGED: bytes copied in, chunks copied as 2-D strides / dense spans / by the gather kernel */
     int registered;   /* this context registered the UMEM (and unregisters it at fini) */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
 };
 
 /* LOWLAT contexts per device in this process (include/xsk_gpu.h, XSK_GPU_LOWLAT_PER_DEVICE): a slot is taken at
- * init and given back at fini; a LOWLAT request without a free slot runs as ZEROCOPY. */
+ * init and given back at fini; a LOWLAT request without a free slot runs as ZEROCOPY.  The cap is the runtime's
+ * highest-priority hardware queues -- min(XSK_GPU_LOWLAT_PER_DEVICE, GPU_MAX_HW_QUEUES), read once -- less the queues
+ * the application reserved for its own highest-priority streams (xsk_gpu_lowlat_reserve). */
 #define LL_MAX_DEV 64
 static atomic_int g_ll_slots[LL_MAX_DEV];
+static atomic_int g_ll_reserved[LL_MAX_DEV];
+static atomic_int g_hw_queues; /* 0: not read yet */
+
+static int hw_queues(void) {
+    int q = atomic_load(&g_hw_queues);
+    if (q > 0) return q;
+    /* the HIP runtime's own variable (its hardware queues per process and priority; HIP's default is 4): not a
+     * switch of this library */
+    const char* e = getenv("GPU_MAX_HW_QUEUES");
+    q = XSK_GPU_LOWLAT_PER_DEVICE;
+    if (e && *e) {
+        char* end = NULL;
+        const long v = strtol(e, &end, 10);
+        if (end != e && v >= 1 && v < q) q = (int)v;
+    }
+    atomic_store(&g_hw_queues, q);
+    return q;
+}
+
+static int ll_cap(int device) {
+    const int cap = hw_queues() - atomic_load(&g_ll_reserved[device]);
+    return cap > 0 ? cap : 0;
+}
 
 static int ll_slot_take(int device) {
     if (device < 0 || device >= LL_MAX_DEV) return 0;
+    const int cap = ll_cap(device);
     int cur = atomic_load(&g_ll_slots[device]);
-    while (cur < XSK_GPU_LOWLAT_PER_DEVICE)
+    while (cur < cap)
         if (atomic_compare_exchange_weak(&g_ll_slots[device], &cur, cur + 1)) return 1;
     return 0;
+}
+
+int xsk_gpu_lowlat_reserve(int device, uint32_t queues) {
+    if (device < 0 || device >= LL_MAX_DEV || queues > XSK_GPU_LOWLAT_PER_DEVICE) return -EINVAL;
+    atomic_store(&g_ll_reserved[device], (int)queues);
+    return ll_cap(device);
 }
 static void ll_slot_give(int device) {
     if (device >= 0 && device < LL_MAX_DEV) atomic_fetch_sub(&g_ll_slots[device], 1);
@@ -97,8 +134,8 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->ll_slot) ll_slot_give(c->device);
-    xsk_gpu__lowlat_free(c->ll);
+    xsk_gpu__lowlat_free(c->ll); /* stops the resident kernel (waits for it) ... */
+    if (c->ll_slot) ll_slot_give(c->device); /* ... before its hardware queue is offered to another context */
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamSynchronize(c->stream[s]);
     if (c->mode == XSK_GPU_MODE_STAGED && c->d_umem) (void)hipFree(c->d_umem);
@@ -117,6 +154,11 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
         for (uint32_t i = 0; i < c->max_chunks; i++)
             if (c->done[i]) (void)hipEventDestroy(c->done[i]);
         free(c->done);
+    }
+    if (c->packed) {
+        for (uint32_t i = 0; i < c->max_chunks; i++)
+            if (c->packed[i]) (void)hipEventDestroy(c->packed[i]);
+        free(c->packed);
     }
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamDestroy(c->stream[s]);
@@ -147,13 +189,14 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     c->max_chunks = mode == XSK_GPU_MODE_STAGED ? (max_batch + CHUNK_FRAMES - 1) / CHUNK_FRAMES : 1;
     TRY(hipSetDevice(device));
     for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamCreateWithFlags(&c->stream[s], hipStreamNonBlocking));
-    if (!prereg) {
-        TRY(hipHostRegister(umem, umem_size, zerocopy(c) ? hipHostRegisterMapped : hipHostRegisterDefault));
+    if (!prereg) { /* mapped in every mode: STAGED's gather kernel reads scattered frames through the alias */
+        TRY(hipHostRegister(umem, umem_size, hipHostRegisterMapped));
         c->registered = 1;
     }
     if (zerocopy(c)) {
         TRY(hipHostGetDevicePointer((void**)&c->d_umem, umem, 0));
     } else {
+        TRY(hipHostGetDevicePointer((void**)&c->m_umem, umem, 0));
         TRY(hipMalloc((void**)&c->d_umem, umem_size));
         TRY(hipMalloc((void**)&c->d_pack, (size_t)max_batch * PACK));
         TRY(hipHostMalloc((void**)&c->h_pack, (size_t)max_batch * PACK, hipHostMallocDefault));
@@ -185,6 +228,15 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
         goto out;
     }
     for (uint32_t i = 0; i < c->max_chunks; i++) TRY(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
+    if (c->mode == XSK_GPU_MODE_STAGED) {
+        c->packed = (hipEvent_t*)calloc(c->max_chunks, sizeof(hipEvent_t));
+        if (!c->packed) {
+            rc = -ENOMEM;
+            goto out;
+        }
+        for (uint32_t i = 0; i < c->max_chunks; i++)
+            TRY(hipEventCreateWithFlags(&c->packed[i], hipEventDisableTiming));
+    }
     if (c->mode == XSK_GPU_MODE_LOWLAT) {
         rc = xsk_gpu__lowlat_start(&c->ll, c->d_umem, umem_size, 0);
         if (rc) goto out;
@@ -205,6 +257,18 @@ int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t ume
 }
 
 uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* c) { return c ? c->max_batch : 0u; }
+
+void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* c) {
+    if (!c || !c->ll) return;
+    (void)hipSetDevice(c->device);
+    xsk_gpu__lowlat_stop(c->ll);
+}
+
+int xsk_gpu__staged_stats(const xsk_gpu_ctx* c, uint64_t out[4]) {
+    if (!c || !out || c->mode != XSK_GPU_MODE_STAGED) return -EINVAL;
+    for (int i = 0; i < 4; i++) out[i] = c->staged[i];
+    return 0;
+}
 int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
 xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
 
@@ -230,32 +294,46 @@ int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     return 0;
 }
 
-/* Copy-in of the bytes the kernel may read for frames d[0..n): [align16(addr), align16(addr)+W) u
- * [addr, addr+len), clipped to the UMEM; W = 64 (128 in wire mode). */
-static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n, hipStream_t st) {
-    uint64_t lo = UINT64_MAX, hi = 0, width = 0;
-    const uint64_t win = c->opts ? WIRE_WIN : 64u;
+/* Copy-in of the bytes the transform reads for frames d[0..n) (xsk_gpu__read_span) into the device mirror, on stream st:
+ *   - a uniform frame stride whose strided rows carry at most 10 % more than those bytes: one 2-D DMA copy;
+ *   - frames covering their span [lo, hi) densely (at most 10 % of it between frames): one DMA copy of the span;
+ *   - otherwise -- AF_XDP's recycled descriptors scatter over the UMEM (xsk_receive.c:55-71, :201-217, :226-227) --
+ *     the gather kernel moves each frame's own bytes across PCIe (dd: the chunk's descriptors, already on the device).
+ * So a call never copies more than 1.1 x the bytes its frames own (c->staged[0] counts them). */
+static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const struct xsk_gpu_desc* dd, uint32_t n,
+                    hipStream_t st) {
+    const int wire = c->opts != 0;
+    uint64_t lo = UINT64_MAX, hi = 0, width = 0, sum = 0;
     for (uint32_t i = 0; i < n; i++) {
-        const uint64_t a = d[i].addr;
-        if (a >= c->umem_size) continue; /* BAD_DESC: the kernel reads nothing */
-        const uint64_t a16 = a & ~15ull;
-        uint64_t e = a + (d[i].len > 48 ? d[i].len : 48);
-        if (e < a16 + win) e = a16 + win;
-        e = (e + 15) & ~15ull;
-        if (e > c->umem_size) e = c->umem_size;
+        uint64_t a16 = 0;
+        const uint64_t sp = xsk_gpu__read_span(d[i].addr, d[i].len, c->umem_size, wire, &a16);
+        if (!sp) continue; /* the transform reads nothing of this frame */
         if (a16 < lo) lo = a16;
-        if (e > hi) hi = e;
-        if (e - a16 > width) width = e - a16;
+        if (a16 + sp > hi) hi = a16 + sp;
+        if (sp > width) width = sp;
+        sum += sp;
     }
-    if (hi <= lo) return 0;
+    if (!sum) return 0;
+    const uint64_t budget = sum + sum / 10;
     const uint64_t s = uniform_stride(d, n);
-    if (s && width <= s && (d[0].addr & ~15ull) + (uint64_t)(n - 1) * s + width <= c->umem_size) {
-        const uint64_t base = d[0].addr & ~15ull;
+    const uint64_t base = d[0].addr & ~15ull;
+    if (s && width <= s && (uint64_t)n * width <= budget && base + (uint64_t)(n - 1) * s + width <= c->umem_size) {
         if (hipMemcpy2DAsync(c->d_umem + base, s, c->umem + base, s, width, n, hipMemcpyHostToDevice, st) != hipSuccess)
             return -EIO;
+        c->staged[0] += (uint64_t)n * width;
+        c->staged[1]++;
         return 0;
     }
-    if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, st) != hipSuccess) return -EIO;
+    if (hi - lo <= budget) {
+        if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, st) != hipSuccess) return -EIO;
+        c->staged[0] += hi - lo;
+        c->staged[2]++;
+        return 0;
+    }
+    const int rc = xsk_gpu__stage_gather_dev(c->m_umem, c->d_umem, c->umem_size, dd, n, (uint32_t)wire, st);
+    if (rc) return rc;
+    c->staged[0] += sum;
+    c->staged[3]++;
     return 0;
 }
 
@@ -279,7 +357,10 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
     TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, st));
     TRY(hipMemsetAsync(c->d_stats + ci, 0, sizeof(struct xsk_gpu_stats), st));
     if (c->mode == XSK_GPU_MODE_STAGED) {
-        rc = stage_in(c, descs + i0, n, st);
+        /* the previous chunk (other stream) has packed its rewritten headers before this copy-in may overwrite
+         * any mirror byte near them */
+        if (ci > 0) TRY(hipStreamWaitEvent(st, c->packed[ci - 1], 0));
+        rc = stage_in(c, descs + i0, dd, n, st);
         if (rc) goto out;
     }
     rc = xsk_gpu_echo_dev_opts(c->d_umem, c->umem_size, dd, n, c->opts, c->d_verdicts + i0,
@@ -289,6 +370,7 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
         rc = xsk_gpu__pack_headers_dev(c->d_umem, dd, c->d_verdicts + i0, n, c->d_pack + (size_t)i0 * PACK,
                                        c->opts != 0, st);
         if (rc) goto out;
+        TRY(hipEventRecord(c->packed[ci], st));
         TRY(hipMemcpyAsync(c->h_pack + (size_t)i0 * PACK, c->d_pack + (size_t)i0 * PACK, (size_t)n * PACK,
                            hipMemcpyDeviceToHost, st));
     }
@@ -317,11 +399,26 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
     }
     if (c->ll && n <= XSK_GPU_LOWLAT_MAX && !no_doorbell) { /* the doorbell: no launch, no sync, no HIP call */
         memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
-        rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL);
-        if (rc) return rc;
-        const uint8_t* hv = xsk_gpu__lowlat_verdicts(c->ll);
-        if (verdicts) memcpy(verdicts, hv, n);
+        uint32_t w = 0, unserved = 0;
+        rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL, &w, &unserved);
+        /* timed out: untouched frames stay the caller's (-ETIMEDOUT) unless the channel stopped with part of the
+         * batch served -- the GPU is evidently alive, so the untouched slices take the launch path and the call
+         * completes, every frame transformed exactly once */
+        const int partial = rc == -ETIMEDOUT && !xsk_gpu__lowlat_broken(c->ll) && unserved &&
+                            unserved != (1u << w) - 1u;
+        if (rc && !partial) return rc;
+        uint8_t hv[XSK_GPU_LOWLAT_MAX];
+        memcpy(hv, xsk_gpu__lowlat_verdicts(c->ll), n);
         if (recs) memcpy(recs, xsk_gpu__lowlat_recs(c->ll), (size_t)n * sizeof *recs);
+        for (uint32_t g = 0; partial && g < w; g++) {
+            if (!((unserved >> g) & 1u)) continue;
+            uint32_t f0 = 0, f1 = 0;
+            xsk_gpu__ll_slice(n, w, g, &f0, &f1);
+            if (f1 <= f0) continue;
+            rc = xsk_gpu__process_ex(c, descs + f0, f1 - f0, hv + f0, recs ? recs + f0 : NULL, NULL, 1);
+            if (rc) return rc;
+        }
+        if (verdicts) memcpy(verdicts, hv, n);
         if (stats) { /* xsk_receive.c:171-172, 229, 233 -- what the kernel's counter phase would add */
             uint64_t rxb = 0, txp = 0, txb = 0;
             for (uint32_t i = 0; i < n; i++) {

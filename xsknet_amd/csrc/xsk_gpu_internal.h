@@ -19,6 +19,32 @@ XSK_GPU__HIDDEN int xsk_gpu__pack_headers_dev(const void* d_umem, const struct x
                                               const uint8_t* d_verdicts, uint32_t n, uint8_t* d_pack, uint32_t wire,
                                               void* stream);
 
+/* The bytes the transform reads of one frame, [*a16, *a16 + return value): for a frame it parses (reference mode:
+ * len >= 20, wire mode: len >= 14, the descriptor inside the UMEM) its 16-B aligned start up to
+ * align16(max(off + len, its header window inside the UMEM)); 0 for a frame it reads nothing of (xsk_echo_device.h,
+ * echo6_body step 1).  Host and device (staged mode's copy-in, xsk_gpu_host.c, and its gather kernel). */
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+static inline uint64_t xsk_gpu__read_span(uint64_t addr, uint32_t len, uint64_t umem_size, int wire, uint64_t* a16) {
+    *a16 = addr & ~15ull;
+    const uint64_t need = wire ? len : (len >= 20u ? (len > 38u ? len : 38u) : len);
+    if (len > XSK_GPU_MAX_LEN || addr > umem_size || need > umem_size - addr || len < (wire ? 14u : 20u)) return 0;
+    const uint64_t off = addr & 15u;
+    const uint64_t win = wire ? 128u : 64u;
+    const uint64_t wend = umem_size - *a16 < win ? umem_size - *a16 : win;
+    const uint64_t lim = off + len > wend ? off + len : wend;
+    return (lim + 15u) & ~15ull;
+}
+
+/* xsk_aux.hip: staged mode's per-frame copy-in for descriptor sets that are neither one uniform stride nor one
+ * dense span (AF_XDP recycles frames through a LIFO free stack, xsk_receive.c:55-71, so RX addresses scatter over the
+ * UMEM): every frame's read span (xsk_gpu__read_span) from the mapped host UMEM into the device mirror at the same
+ * offset.  d_descs in device memory. */
+XSK_GPU__HIDDEN int xsk_gpu__stage_gather_dev(const void* m_umem, void* d_mirror, uint64_t umem_size,
+                                              const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t wire,
+                                              void* stream);
+
 /* xsk_echo.hip: xsk_gpu_echo_dev_opts for counters in mapped host memory (no device atomics): d_stats
  * must be a slot zeroed for this call (a one-workgroup launch stores the counters without reading it).
  * tile: frames per wave of a small batch (xsk_gpu__small_tile), 0 = ceil(n / 16). */
@@ -90,6 +116,13 @@ int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 XSK_GPU__HIDDEN int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size,
                                          uint32_t max_batch, int mode);
 XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
+/* xsk_gpu_host.c: stop the context's resident LOWLAT kernel, if any, and wait for it (the multi-context path stops
+ * every context's before a batch whose shares take the launch path). */
+XSK_GPU__HIDDEN void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* ctx);
+/* xsk_gpu_host.c (exported for the GPU tests, not part of the ABI): a STAGED context's copy-in record since init --
+ * out[0] bytes copied host->device, out[1..3] chunks copied as one 2-D stride / one dense span / by the gather
+ * kernel.  -EINVAL for other modes. */
+int xsk_gpu__staged_stats(const xsk_gpu_ctx* ctx, uint64_t out[4]);
 
 /* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context (doorbell layout and
  * host protocol: xsk_lowlat_proto.h). */
@@ -112,8 +145,11 @@ typedef struct xsk_gpu__lowlat xsk_gpu__lowlat;
  * buffers and stream.  The persistent kernel starts with the first batch. */
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_size, uint32_t opts);
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll);
-/* Post the batch already written into the mapped descriptor buffer and wait for its completion. */
-XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs);
+/* Post the batch already written into the mapped descriptor buffer and wait for its completion (xsk_gpu__ll_run):
+ * *groups = the workgroups it was posted for (its slices: xsk_gpu__ll_slice), and on -ETIMEDOUT *unserved = the
+ * slices left untouched (all bits when the channel is broken: unknown). */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups,
+                                        uint32_t* unserved);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts);
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
 /* 1 while a timed-out batch's instance has not stopped (later calls return -EBUSY). */

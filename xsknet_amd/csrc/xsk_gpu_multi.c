@@ -53,7 +53,9 @@ struct xsk_gpu_multi {
     uint32_t job_n;
     uint8_t* job_verd;
     struct xsk_gpu_rec* job_recs;
-    int job_launch; /* every share takes the launch path (a share above XSK_GPU_LOWLAT_MAX) */
+    int job_launch; /* every share takes the launch path (a share above XSK_GPU_LOWLAT_MAX, or not every context
+                     * runs LOWLAT) */
+    int all_lowlat; /* every context really runs XSK_GPU_MODE_LOWLAT (none was downgraded at init) */
     int status[XSK_GPU_MULTI_MAX]; /* per-context result of the last xsk_gpu_multi_process */
 };
 
@@ -166,6 +168,8 @@ int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, v
         rc = xsk_gpu__init_prereg(&w->ctx, devices[g], umem, umem_size, cap, mode);
         if (rc) goto fail;
     }
+    m->all_lowlat = 1;
+    for (uint32_t g = 0; g < ndev; g++) m->all_lowlat &= xsk_gpu_ctx_mode(m->w[g].ctx) == XSK_GPU_MODE_LOWLAT;
     for (uint32_t g = 1; g < ndev; g++) {
         if (pthread_create(&m->w[g].th, NULL, worker_main, &m->w[g]) != 0) {
             rc = -EAGAIN;
@@ -198,9 +202,13 @@ int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, ui
     m->job_n = n;
     m->job_verd = verdicts;
     m->job_recs = recs;
-    /* the path is chosen per batch, not per share: when any share is too large for a LOWLAT doorbell, every
-     * context takes the launch path, so no share runs on a CU that a resident kernel holds */
-    m->job_launch = (n + m->G - 1) / m->G > XSK_GPU_LOWLAT_MAX;
+    /* the path is chosen per batch from the modes the contexts really run, not per share: the doorbell only when
+     * every context runs LOWLAT (a LOWLAT request beyond the device's resident-kernel cap runs as ZEROCOPY) and every
+     * share fits it; otherwise every context takes the launch path, and every resident kernel has stopped before
+     * any share is launched, so no share runs beside a resident kernel that holds a CU */
+    m->job_launch = !m->all_lowlat || (n + m->G - 1) / m->G > XSK_GPU_LOWLAT_MAX;
+    if (m->job_launch)
+        for (uint32_t g = 0; g < m->G; g++) xsk_gpu__ctx_quiesce(m->w[g].ctx);
     if (m->G > 1) {
         pthread_mutex_lock(&m->mu);
         m->pending = m->G - 1;

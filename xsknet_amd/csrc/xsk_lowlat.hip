@@ -127,6 +127,17 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
                 P.served = (uint32_t)c;
                 return 0;
             }
+            if (c & XSK_GPU__BELL_STOP) {
+                // posted, then cancelled before this workgroup took it (its call timed out, e.g. while this instance
+                // was still queued): retire it WITHOUT serving -- the host then knows the slice is untouched
+                // (xsk_gpu__ll_unserved) and the caller's retry transforms it exactly once
+                P.served = (uint32_t)c;
+                if (lane == 0) {
+                    st_sys(&bell->wg[g].cancel, (uint32_t)c);
+                    st_sys(&bell->wg[g].done, (uint32_t)c);
+                }
+                return 2;
+            }
             if (LEADER && w == 1u && nn <= (uint32_t)kTile) {
                 if (__ballot(lane < nn && (uint32_t)(d1 >> 32) != (uint32_t)c) != 0ull) {
                     ++P.n_stale;
@@ -345,6 +356,7 @@ int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll) {
     if (!ll || !ll->st.broken) return 1;
     (void)hipSetDevice(ll->device);
     if (!ll_stream_idle(ll)) return 0;
+    xsk_gpu__ll_retire(&ll->st);  // the stopped instance's batch is never served by a relaunch
     ll->st.broken = 0;
     ll->st.launched = 0;
     return 1;
@@ -422,7 +434,9 @@ int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts) {
     return 0;
 }
 
-int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
+int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups, uint32_t* unserved) {
+    if (groups) *groups = 0;
+    if (unserved) *unserved = 0;
     if (!ll || n > XSK_GPU_LOWLAT_MAX) return -EINVAL;
     const double h_enter = ll_now(nullptr);
     if (ll->st.broken && !ll_stream_idle(ll)) return -EBUSY;  // before touching the slots it may still read
@@ -441,8 +455,10 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs) {
     }
     const xsk_gpu__ll_ops o = ll_ops(ll);
     const double h_post = ll_now(nullptr);
+    if (groups) *groups = w;
     const int rc = xsk_gpu__ll_run(&ll->st, &o,
-                                   XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) | XSK_GPU__BELL_TILE(tq), w);
+                                   XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) | XSK_GPU__BELL_TILE(tq), w,
+                                   unserved);
     if (rc) return rc;
     const double h_done = ll_now(nullptr);
     ll->host_ns[0] = (uint64_t)((h_post - h_enter) * 1e9);

@@ -56,11 +56,13 @@ struct xsk_gpu__bell {
         uint32_t pad[14];
     } wcmd[XSK_GPU__LL_WG - 1];
     /* device -> host, one line per workgroup: seq of the last batch it completed (its slice written back);
-     * wg[0].alive = 1 while the leader runs */
+     * wg[0].alive = 1 while the leader runs; cancel = seq of a batch the workgroup found already cancelled (STOP
+     * in the same command word) and retired WITHOUT serving it (then done == cancel too) */
     struct {
         volatile uint32_t done;
         volatile uint32_t alive;
-        uint32_t pad[14];
+        volatile uint32_t cancel;
+        uint32_t pad[13];
     } wg[XSK_GPU__LL_WG];
 };
 
@@ -106,6 +108,8 @@ struct xsk_gpu__ll_ops {
 struct xsk_gpu__ll_state {
     struct xsk_gpu__bell* bell;
     uint32_t seq;         /* last posted batch */
+    uint64_t cmd;         /* its whole command word (a STOP keeps its n / workgroup fields) */
+    uint32_t stop_unserved; /* the last ll_stop that found the grid stopped: xsk_gpu__ll_unserved of the last batch */
     int launched;         /* an instance was launched and may still run */
     int broken;           /* a timed-out batch whose instance had not stopped when the call returned */
     double timeout_s;     /* a batch not complete after this long: -ETIMEDOUT */
@@ -119,15 +123,39 @@ static inline void xsk_gpu__ll_post(struct xsk_gpu__bell* b, uint64_t c) {
     __atomic_store_n(&b->cmd, c, __ATOMIC_SEQ_CST);
 }
 
-/* Stop the resident grid (xsk_gpu_fini, a large batch, new options): post STOP keeping the last seq, and
- * wait up to `wait_s` (< 0: for ever) for the stream to drain.  Returns 0 once no instance runs, -ETIMEDOUT
- * if one still did at the deadline (the channel is then `broken`). */
+/* No instance runs (its stream is idle): retire the last posted batch for every workgroup, so that a relaunched grid
+ * -- whose workgroups take their baselines from `done` -- never serves a batch whose call has already returned
+ * (the launch re-posts the command word without its STOP bit). */
+static inline void xsk_gpu__ll_retire(struct xsk_gpu__ll_state* st) {
+    for (uint32_t g = 0; g < XSK_GPU__LL_WG; g++) __atomic_store_n(&st->bell->wg[g].done, st->seq, __ATOMIC_SEQ_CST);
+}
+
+/* Slices of the last posted batch (w serving workgroups) that were NOT transformed: bit g set when workgroup g never
+ * completed seq or retired it unserved (cancel == seq).  Meaningful once no instance runs. */
+static inline uint32_t xsk_gpu__ll_unserved(const struct xsk_gpu__bell* b, uint32_t seq, uint32_t w) {
+    uint32_t m = 0;
+    for (uint32_t g = 0; g < w; g++)
+        if (__atomic_load_n(&b->wg[g].done, __ATOMIC_ACQUIRE) != seq ||
+            __atomic_load_n(&b->wg[g].cancel, __ATOMIC_ACQUIRE) == seq)
+            m |= 1u << g;
+    return m;
+}
+
+/* Stop the resident grid (xsk_gpu_fini, a large batch, new options, a timeout): post STOP in the last command
+ * word (its seq, n and workgroup fields kept, so a workgroup that has not taken that batch yet retires exactly its
+ * own slice unserved), and wait up to `wait_s` (< 0: for ever) for the stream to drain.  Returns 0 once no instance
+ * runs -- the last batch then retired for every workgroup -- or -ETIMEDOUT if one still did at the deadline (the
+ * channel is then `broken`). */
 static inline int xsk_gpu__ll_stop(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, double wait_s) {
     if (!st->launched && !st->broken) return 0;
-    xsk_gpu__ll_post(st->bell, (uint64_t)st->seq | XSK_GPU__BELL_STOP);
+    xsk_gpu__ll_post(st->bell, (st->cmd & ~0xFFFFFFFFull) | (uint64_t)st->seq | XSK_GPU__BELL_STOP);
     const double t0 = ops->now(ops->u);
     for (;;) {
         if (ops->stream_idle(ops->u)) {
+            uint32_t w = (uint32_t)(st->cmd >> 56) & 7u;
+            w = w < 1u ? 1u : (w > XSK_GPU__LL_WG ? XSK_GPU__LL_WG : w);
+            st->stop_unserved = xsk_gpu__ll_unserved(st->bell, st->seq, w); /* what the workgroups did, then: */
+            xsk_gpu__ll_retire(st);
             st->launched = 0;
             st->broken = 0;
             return 0;
@@ -146,15 +174,20 @@ static inline int xsk_gpu__ll_stop(struct xsk_gpu__ll_state* st, const struct xs
  * then in the mapped buffers), or:
  *   -EBUSY      an earlier call timed out and its instance has still not stopped: nothing was posted;
  *   -ETIMEDOUT  the batch did not complete within timeout_s: STOP was posted and the instance waited for
- *               (quiesce_s); once it has stopped the caller owns its frames again (the batch may or may not
- *               have been transformed), else the channel stays `broken` and later calls return -EBUSY until
- *               it has;
+ *               (quiesce_s).  Once it has stopped, every slice is either transformed exactly once or untouched
+ *               (a workgroup that finds STOP with a batch it has not taken retires it unserved), *unserved says
+ *               which slices are untouched (bit g: slice g of xsk_gpu__ll_slice), and no later instance serves the
+ *               batch; if every slice turned out to be served the call returns 0 after all.  If the instance had not
+ *               stopped by then, the channel stays `broken`, *unserved has every bit set (unknown), and later calls
+ *               return -EBUSY until it has;
  *   a launch error. */
 static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, uint64_t bits,
-                                  uint32_t w) {
+                                  uint32_t w, uint32_t* unserved) {
     struct xsk_gpu__bell* b = st->bell;
+    if (unserved) *unserved = 0;
     if (st->broken) {
         if (!ops->stream_idle(ops->u)) return -EBUSY;
+        xsk_gpu__ll_retire(st); /* the stopped instance's batch is never served by a relaunch */
         st->broken = 0;
         st->launched = 0;
     }
@@ -168,7 +201,8 @@ static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk
     }
     const uint32_t seq = st->seq + 1u;
     st->seq = seq;
-    xsk_gpu__ll_post(b, (uint64_t)seq | bits | XSK_GPU__BELL_WG(w));
+    st->cmd = (uint64_t)seq | bits | XSK_GPU__BELL_WG(w);
+    xsk_gpu__ll_post(b, st->cmd);
     if (!fresh && !__atomic_load_n(&b->wg[0].alive, __ATOMIC_SEQ_CST)) {
         /* the leader was leaving (Dekker: it re-reads the doorbell after clearing alive, or this launch serves
          * the batch) */
@@ -197,8 +231,14 @@ static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk
                 }
             }
             if (t - t_post > st->timeout_s) {
-                (void)xsk_gpu__ll_stop(st, ops, st->quiesce_s);
-                return -ETIMEDOUT;
+                if (xsk_gpu__ll_stop(st, ops, st->quiesce_s) != 0) { /* still running: broken, outcome unknown */
+                    if (unserved) *unserved = (1u << w) - 1u;
+                    return -ETIMEDOUT;
+                }
+                /* (ll_stop recorded what the workgroups did with the batch before it retired it) */
+                if (unserved) *unserved = st->stop_unserved;
+                if (st->stop_unserved) return -ETIMEDOUT;
+                break; /* every slice was served, late: a normal completion */
             }
         }
         ops->relax(ops->u);
