@@ -81,7 +81,7 @@ def packed(lens, seed):
                              threads=min(16, oracle.cpu_threads()))
     gen["len"] = lens  # (synth's own lengths are uniform in [lo, hi]; set ours and fix the headers below)
     base = np.concatenate([[0], np.cumsum(lens.astype(np.int64))[:-1]])
-    umem = np.zeros(int(base[-1] + lens[-1]) + 4096, np.uint8)
+    umem = np.zeros((int(base[-1] + lens[-1]) + 4096 + 15) & ~15, np.uint8)  # (the ABI wants a multiple of 16)
     descs = np.zeros(n, X.DESC_DTYPE)
     for j in range(n):
         umem[base[j]:base[j] + lens[j]] = tmp[j * 2048:j * 2048 + lens[j]]
