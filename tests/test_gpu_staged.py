@@ -114,7 +114,8 @@ def test_staged_multi_chunk_overlapping_spans():
 def test_staged_copy_in_paths():
     """The three copy-in paths each on the layout that picks it, exact: a uniform 4 KiB stride of 1500-B frames (one
     2-D copy per chunk), packed frames of mixed lengths (one dense span), and the same mixed frames at a uniform 2 KiB
-    stride, where the strided rows would carry 2 x the frames' bytes (the gather kernel)."""
+    stride, where the strided rows would carry 2 x the frames' bytes (the gather kernel); an RX-loop-sized batch
+    (<= 1024 frames) always takes the gather kernel."""
     _dev()
     cases = []
     n = 5000
@@ -134,6 +135,12 @@ def test_staged_copy_in_paths():
         check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
         assert rec[path] == 1 and sum(rec[k] for k in ("strided", "span", "gather")) == 1, (path, rec)
         assert rec["h2d_bytes"] <= 1.1 * owned_bytes(descs), (path, rec, owned_bytes(descs))
+        work = umem.copy()
+        with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_STAGED) as ctx:
+            v, r, tot = run_batches(ctx, descs[:3000], 1000)
+            rec = ctx.staged_stats()
+        check(umem, work, descs[:3000], v, r, tot)
+        assert rec["gather"] == 3 and rec["strided"] == 0 and rec["span"] == 0, (path, rec)
 
 
 def test_staged_scrambled_multi_context():

@@ -295,6 +295,7 @@ int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
 }
 
 /* Copy-in of the bytes the transform reads for frames d[0..n) (xsk_gpu__read_span) into the device mirror, on stream st:
+ *   - n <= XSK_GPU_LOWLAT_MAX (an RX-loop batch): the gather kernel below, whatever the layout;
  *   - a uniform frame stride whose strided rows carry at most 10 % more than those bytes: one 2-D DMA copy;
  *   - frames covering their span [lo, hi) densely (at most 10 % of it between frames): one DMA copy of the span;
  *   - otherwise -- AF_XDP's recycled descriptors scatter over the UMEM (xsk_receive.c:55-71, :201-217, :226-227) --
@@ -317,14 +318,18 @@ static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const struct x
     const uint64_t budget = sum + sum / 10;
     const uint64_t s = uniform_stride(d, n);
     const uint64_t base = d[0].addr & ~15ull;
-    if (s && width <= s && (uint64_t)n * width <= budget && base + (uint64_t)(n - 1) * s + width <= c->umem_size) {
+    /* an RX-loop-sized batch takes the gather kernel whatever its layout: one launch beats a DMA submission there
+     * (64 x 64 B: 55.7 us per call vs 66.1 with the 2-D copy; 1024 x 1500 B: 126.2 vs 129.0 --
+     * profiles/r04/pass1/hostlat_*.jsonl) */
+    const int small = n <= XSK_GPU_LOWLAT_MAX;
+    if (!small && s && width <= s && (uint64_t)n * width <= budget && base + (uint64_t)(n - 1) * s + width <= c->umem_size) {
         if (hipMemcpy2DAsync(c->d_umem + base, s, c->umem + base, s, width, n, hipMemcpyHostToDevice, st) != hipSuccess)
             return -EIO;
         c->staged[0] += (uint64_t)n * width;
         c->staged[1]++;
         return 0;
     }
-    if (hi - lo <= budget) {
+    if (!small && hi - lo <= budget) {
         if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, st) != hipSuccess) return -EIO;
         c->staged[0] += hi - lo;
         c->staged[2]++;
