@@ -14,8 +14,9 @@ pytestmark = pytest.mark.gpu
 import xsknet_amd as X  # noqa: E402
 
 # 0 as shipped (reference), 2 wire mode as shipped, 3 / 4 ranked streams with 4 / 8 row-loads per batch, 5 / 6 no SPLIT
-# (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4
-VARIANTS = [0, 2, 3, 4, 5, 6, 7, 8, 9, 13]
+# (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4, 14 / 15 / 16 lean ranked streams (RS 2) with
+# 6 / 8 / 4 row-loads per batch
+VARIANTS = [0, 2, 3, 4, 5, 6, 7, 8, 9, 13, 14, 15, 16]
 WIRE_VARIANTS = (2, 6, 8)
 
 

@@ -105,6 +105,10 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         // 9: SLACK 0 -- heavy waves wait for every wave of the workgroup (round 3's write-phase wait); 13: SLACK 4
         case 9: echo_round_kernel<false, false, kUR, true, true, 0><<<gg, bb, 0, s>>>(args, per); break;
         case 13: echo_round_kernel<false, false, kUR, true, true, 4><<<gg, bb, 0, s>>>(args, per); break;
+        // 14 / 15 / 16: RS 2 -- the lean ranked streams (stream_tile_ranked2) with 6 / 8 / 4 row-loads per batch
+        case 14: echo_round_kernel<false, false, kUR, true, true, kRefSlack, 2><<<gg, bb, 0, s>>>(args, per); break;
+        case 15: echo_round_kernel<false, false, 8, true, true, kRefSlack, 2><<<gg, bb, 0, s>>>(args, per); break;
+        case 16: echo_round_kernel<false, false, 4, true, true, kRefSlack, 2><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

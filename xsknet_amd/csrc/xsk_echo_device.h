@@ -389,6 +389,121 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
     }
 }
 
+// Ranked streams, lean form (RS 2; the tile's frames within a 2 GiB buffer window and <= 64 KiB).  The same schedule as
+// stream_tile_sorted -- frames ranked by row-load count, step s = ranks 4s..4s+3, U row-loads per batch packed across
+// steps -- at a fraction of its instructions per row-load (round 3 counted ~300 to issue a batch of six: a readlane and
+// a dozen scalar ops per slot, and per new step two DEPENDENT LDS reads, rank -> frame -> metadata, before the step's
+// address):
+//   - each lane writes its frame's metadata to the slot of its RANK (meta[] is overwritten in rank order; the 16-B
+//     entry carries the frame's own index for the window and the sum), so a step's row reads ONE broadcast entry;
+//   - the batch's entries are read together, one LDS wait per batch, before any address work;
+//   - the slot cursor keeps the current step's row-load count in a scalar (a readlane only when a step begins);
+//   - sums are 32-bit sums of 16-bit halves (v_dot2_u32_u16, no 64-bit carries, no fold), masked only in the block a
+//     frame ends in and in row-load 0 (the window and the ICMP start).
+// The frame-of-rank index and the step row-load counts use the sort row as stream_tile_sorted does.
+template <int U, bool PRIO>
+__device__ __forceinline__ void stream_tile_ranked2(__amdgpu_buffer_rsrc_t rsrc, FrameMeta6* meta, uint32_t* sort,
+                                                    uint8_t* rows, uint32_t* sums_ic, uint32_t nit_own, uint32_t rel_own,
+                                                    uint32_t rowhi_own, uint32_t lim_own, uint32_t off_own,
+                                                    uint32_t lane) {
+    const uint32_t q = lane >> 4, k = lane & 15u;
+    uint32_t rank = 0;
+    if (__ballot(nit_own > 7u) == 0ull) {  // counting rank (one ballot per value), as stream_tile_sorted
+        uint32_t below = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < 8u; ++v) {
+            const uint64_t bv = __ballot(nit_own == v);
+            const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(bv >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bv, 0u));
+            if (nit_own == v) rank = below + mb;
+            below += (uint32_t)__popcll(bv);
+        }
+    } else {
+        for (uint32_t j = 0; j < 64u; ++j) {
+            const uint32_t nj = rdlane(nit_own, j);
+            rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
+        }
+    }
+    // the tile's metadata in rank order (lane = frame wrote meta[lane] before; every lane rewrites one entry, a
+    // permutation, in one wave instruction) -- .packed = off | frame << 8
+    {
+        FrameMeta6 m;
+        m.rel = rel_own;
+        m.rowhi = rowhi_own;
+        m.lim = lim_own;
+        m.packed = off_own | (lane << 8);
+        meta[rank] = m;
+    }
+    if ((rank & 3u) == 3u) sort[64u + (rank >> 2)] = nit_own;  // sort[64 + s]: row-loads of step s
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t stepns = sort[64u + (lane & 15u)];  // lane s (< 16): row-loads of step s
+    uint32_t s = 0;
+    while (s < 16u && rdlane(stepns, s) == 0u) ++s;
+    uint32_t ns = s < 16u ? rdlane(stepns, s) : 0u, j = 0;  // the cursor: step s, its row-loads, row-load j
+    uint32_t cur = 16u, cur_f = 0u, h = 0u;                   // the step being summed, its frame (per row), sum
+    while (s < 16u) {
+        uint32_t us[U], uj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // wave-uniform slot assignment
+            us[u] = s;
+            uj[u] = j;
+            if (s < 16u && ++j >= ns) {
+                ++s;
+                j = 0;
+                ns = s < 16u ? rdlane(stepns, s) : 0u;
+            }
+        }
+        FrameMeta6 fm[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)  // every slot's entry (slots of one step read the same one: a broadcast)
+            if (us[u] < 16u) fm[u] = meta[4u * us[u] + q];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        u32x4 v[U];
+        if (PRIO) __builtin_amdgcn_s_setprio(2);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = u32x4{0u, 0u, 0u, 0u};
+            if (us[u] < 16u) {
+                const uint32_t ro = 256u * uj[u] + 16u * k;
+                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ro < fm[u].lim ? fm[u].rel + ro : 0x80000000u), 0,
+                                                             kAuxNT);
+            }
+        }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (us[u] >= 16u) continue;  // uniform
+            if (us[u] != cur) {          // uniform: a new step begins in this slot
+                if (cur < 16u) {
+                    const uint32_t r = row_sum_dpp(h);
+                    if (k == 15u) sums_ic[cur_f] = r;
+                }
+                cur = us[u];
+                cur_f = fm[u].packed >> 8;
+                h = 0u;
+            }
+            const uint32_t ro = 256u * uj[u] + 16u * k;
+            u32x4 x = v[u];
+            const int hi = (int)fm[u].rowhi;
+            if (uj[u] == 0u) {
+                if (k < 4u && fm[u].lim) *(u32x4*)(rows + cur_f * (uint32_t)kWin + ro) = x;  // the header window
+                x &= range_mask((int)ro, (int)(fm[u].packed & 0xFFu) + 34, hi);
+            } else if (__ballot((int)ro < hi && hi < (int)ro + 16) != 0ull) {  // a block some row's frame ends in
+                const int nb = hi - (int)min(ro, (uint32_t)hi);
+                x.x &= dw_mask(nb);
+                x.y &= dw_mask(nb - 4);
+                x.z &= dw_mask(nb - 8);
+                x.w &= dw_mask(nb - 12);
+            }
+            h = sum_halves(x, h);
+        }
+    }
+    if (cur < 16u) {
+        const uint32_t r = row_sum_dpp(h);
+        if (k == 15u) sums_ic[cur_f] = r;
+    }
+}
+
 // Uniform long tiles: every frame of the tile parsed, at the same 16-B offset and with the same end, so
 // the ICMP byte range [lo, hi) = [off + 34, off + len) is the same in every row.  A lane's byte masks are
 // then the same for every step: computed once per tile for the first and the last row-load (the only blocks
@@ -866,7 +981,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1046,7 +1161,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     } else if (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                uniform(max_nit_lane(nit)) < (uint32_t)U) {
                         // ragged tile (or one too short to fill a batch of U row-loads): ranked streams
-                        if (fast) stream_tile_sorted<UR, true, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        if (RS == 2 && REF && fast && uniform(max_nit_lane(nit)) <= 257u)
+                            stream_tile_ranked2<UR, PRIO>(ld.r, meta, sm.sort[wave], rows, sums_ic, nit,
+                                                          nit ? (uint32_t)(a16 - wlo) : 0u, rowhi, lim, off, lane);
+                        else if (fast) stream_tile_sorted<UR, true, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                         else stream_tile_sorted<UR, false, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
                         stream_tile_uniform<U, WIRE, USPLIT, PRIO>(ld.r, meta, rows, sums_ic, uniform(nit),
@@ -1165,7 +1283,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack>
+          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack, int RS = 1>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1174,7 +1292,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
     echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
-               SLACK>(a, t_begin, t_end, sm);
+               SLACK, RS>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
