@@ -1,16 +1,12 @@
-# Cold A/B of tuning-library kernel variants inside one GPU call (run through gpurun): every variant of
-# every config timed by bench.py --variant in its own process, the variants interleaved per repetition so
-# that box drift hits them alike; prints one "config variant kernel_avg_us" line per run.
-#   bash tools/gpu_ab.sh <out-dir> <configs,comma> <variants,comma> <reps>
+# In-process A/B of product-switch variants (tools/abbench.py), after their parity tests.
+#   bash tools/gpu_ab.sh <tag> <variants> <rounds> <configs...>      e.g. bash tools/gpu_ab.sh r04b -1,14 6 c4 c3
 cd "$GRAFT_REPO_ROOT" || exit 3
-O=$1; CFGS=$2; VARS=$3; REPS=${4:-2}
+O=gpurun_out/$1; V=$2; R=$3; shift 3
 mkdir -p $O
-for r in $(seq 1 $REPS); do
-  for c in ${CFGS//,/ }; do
-    for v in ${VARS//,/ }; do
-      f=$O/b_${v}_${c}_$r.json
-      timeout -k 10 240 python bench.py --config $c --variant $v --steps 20 --warmup 3 --no-cpu > $f 2> $O/b_${v}_${c}_$r.err || { echo "FAIL $c $v rc=$?"; exit 1; }
-      python3 -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$c', $v, d['roofline']['kernel_avg_us'], d['ms_per_step'])"
-    done
-  done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_tune.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tune_tests.log 2>&1 || { tail -5 $O/tune_tests.log; exit 1; }
+tail -1 $O/tune_tests.log
+for c in "$@"; do
+  timeout -k 10 400 python -u tools/abbench.py --config $c --variants=$V --rounds $R > $O/ab_$c.log 2>&1 || { tail -3 $O/ab_$c.log; exit 1; }
+  tail -1 $O/ab_$c.log | cut -c1-400
 done
+echo done
