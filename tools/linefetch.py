@@ -27,6 +27,8 @@ def useful_bytes(mode, nbytes):
         return nbytes // 2
     if mode == 2:
         return nbytes // 8
+    if mode == 7:
+        return nbytes
     import numpy as np
     j = np.arange(nbytes // 2048, dtype=np.uint64)
     with np.errstate(over="ignore"):
@@ -37,6 +39,8 @@ def useful_bytes(mode, nbytes):
     ln = 64 + (z % np.uint64(1437)).astype(np.int64)
     if mode == 4:
         ln = (ln + 127) // 128 * 128
+    if mode in (5, 6, 8):  # whole 16-B blocks of each frame
+        ln = (ln + 15) // 16 * 16
     return int(ln.sum())
 
 

@@ -981,7 +981,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1224,7 +1224,10 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         if (SYNC == 2) {
             ++rounds_done;
             if (lane == 0) atomicAdd(&s_arrive, 1u);
-            if (uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
+            // LASTW: in the share's last round no wave waits -- its writes have no later reads of this workgroup to
+            // stay out of the way of, and the kernel's tail is that round's write phase
+            if ((LASTW == 0 || r0 + kRound < t_end) &&
+                uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
                 // (every wave but SLACK: the last waves of a round are usually ragged ones still streaming)
                 while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
                        rounds_done * (uint32_t)kWaves6 - (uint32_t)SLACK)
@@ -1283,7 +1286,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack, int RS = 1>
+          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack, int RS = 1, int LASTW = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1292,7 +1295,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
     echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
-               SLACK, RS>(a, t_begin, t_end, sm);
+               SLACK, RS, LASTW>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
