@@ -57,10 +57,11 @@ def _dev():
 
 @pytest.mark.parametrize("mode,ctx_batch,step_batch", [(X.MODE_ZEROCOPY, 1024, 64), (X.MODE_STAGED, 1024, 64),
                                                       (X.MODE_LOWLAT, 1024, 64), (X.MODE_LOWLAT, 64, 1024),
-                                                      (X.MODE_ZEROCOPY, 64, 1024)])
+                                                      (X.MODE_ZEROCOPY, 64, 1024), (X.MODE_STAGED, 1024, 1024)])
 def test_rx_loop_end_to_end(mode, ctx_batch, step_batch):
     """ctx_batch < step_batch: the step peeks no more than the context takes (never an -EINVAL after the
-    fill ring was restocked)."""
+    fill ring was restocked).  The free stack recycles frames LIFO (xsk_receive.c:55-71), so after the first wrap
+    every step's addresses are scattered over the UMEM: STAGED steps of up to 1024 frames take the gather copy-in."""
     _dev()
     n_pkts, seed = 20000, 0x5EED0A0A
     umem = np.zeros(NUM_FRAMES * FRAME_SIZE, np.uint8)

@@ -143,6 +143,26 @@ def test_staged_copy_in_paths():
         assert rec["gather"] == 3 and rec["strided"] == 0 and rec["span"] == 0, (path, rec)
 
 
+def test_staged_scrambled_wire_mode():
+    """Wire mode (every option: 128-B header windows, so every frame's read span is at least 128 B) on scrambled
+    descriptors over two chunks and on 64-frame calls: exact against the wire oracle, copy-in = the wire read spans."""
+    _dev()
+    n = CHUNK + 4321
+    umem, descs = scrambled(n, n + 1000, 2048, 0, 0x5EED4E4F, mode=1, lo=20, hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
+    for batch in (n, 64):
+        work = umem.copy()
+        with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_STAGED, opts=X.OPT_ALL) as ctx:
+            v, r, tot = run_batches(ctx, descs, batch)
+            rec = ctx.staged_stats()
+        assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all(), batch
+        for k in COUNTERS:
+            assert tot[k] == int(s_ref[k]), (batch, k)
+        spans = sum(read_span(int(a), int(ln), umem.nbytes, wire=True) for a, ln in zip(descs["addr"], descs["len"]))
+        assert rec["h2d_bytes"] == spans, (batch, rec, spans)
+
+
 def test_staged_scrambled_multi_context():
     """The same scrambled descriptor sets through xsk_gpu_multi G = 2 (two STAGED contexts on the one GPU, one
     registration, descriptor i on context i mod 2): exact."""
