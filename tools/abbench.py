@@ -98,7 +98,28 @@ def main():
             times[v].append(e0.elapsed_time(e1) * 1000.0 / m)
         print(json.dumps({"round": r, **{str(v): round(float(np.median(times[v][-max(1, len(evs) // len(V)):])), 2)
                                          for v in V}}), flush=True)
-    out = {"config": args.config, "pool": pool, "rounds": args.rounds, "desc": desc}
+    # every variant's outputs against the shipped entry point's on one fresh batch: slab, verdicts, records (a variant
+    # that skips a store would otherwise time faster and pass unnoticed)
+    regen()
+    ref_u = slab[:bb].clone()
+    ref_v = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
+    ref_r = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    X.echo_dev(ref_u, descs[0], n, ref_v, ref_r, stats, ws, stream)
+    verified = {}
+    for v in V:
+        u = slab[bb:2 * bb] if pool > 1 else slab[:bb]
+        u.copy_(slab[:bb] if pool > 1 else ref_u)  # (pool of one: compare the shipped kernel with itself)
+        verd.fill_(0xEE)
+        recs.zero_()
+        if v < 0:
+            X.echo_dev(u, descs[0], n, verd, recs, stats, ws, stream)
+        else:
+            rc = tune.xsk_gpu__product_variant(v % 1000, 0, u.data_ptr(), u.numel(), descs[0].data_ptr(), n,
+                                               verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
+            assert rc == 0, rc
+        torch.cuda.synchronize()
+        verified[str(v)] = bool(torch.equal(u, ref_u) and torch.equal(verd, ref_v) and torch.equal(recs, ref_r))
+    out = {"config": args.config, "pool": pool, "rounds": args.rounds, "desc": desc, "outputs_equal_shipped": verified}
     for v in V:
         t = np.sort(np.array(times[v]))
         k = len(t) // 8

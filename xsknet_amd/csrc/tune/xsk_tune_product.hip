@@ -112,10 +112,6 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         // 17: LASTW -- no write-phase wait in the share's last round (reference mode); 18: the same in wire mode
         case 17: echo_round_kernel<false, false, kUR, true, true, kRefSlack, 1, 1><<<gg, bb, 0, s>>>(args, per); break;
         case 18: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0, 1, 1><<<gg, bb, 0, s>>>(args, per); break;
-        // 19: EARLY -- records and verdicts stored right after each tile's header phase instead of in the write phase
-        // (the write phase then carries only the scattered windows); 20: the same in wire mode
-        case 19: echo_round_kernel<false, false, kUR, true, true, kRefSlack, 1, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
-        case 20: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0, 1, 0, 1><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

@@ -953,26 +953,6 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
     return true;
 }
 
-// A tile's records (coalesced 16-B stores, write-through under WT) and verdicts.
-template <bool SUBT, bool WT>
-__device__ __forceinline__ void store_rec_verd(const EchoArgs& a, uint32_t t, uint32_t t_end, u32x4 rec, uint32_t verd,
-                                               uint32_t lane) {
-    if (t >= t_end) return;  // wave-uniform
-    const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
-    if ((!SUBT || lane < a.tile_live) && fi < a.n) {
-        if (a.recs) {
-            if (WT)
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    rec,
-                    __builtin_amdgcn_make_buffer_rsrc((void*)((u32x4*)a.recs + (uint64_t)uniform(t) * (SUBT ? a.tile_live : (uint32_t)kTile)),
-                                                      (short)0, -1, kRsrcFlags),
-                    (int)(lane * 16u), 0, kAuxSC1);
-            else ((u32x4*)a.recs)[fi] = rec;
-        }
-        if (a.verdicts) a.verdicts[fi] = (uint8_t)verd;
-    }
-}
-
 // ================================================================================================
 // The round kernel.  Measured on cold 4 GiB slabs (tools/wexp.hip): a read stream that meets scattered
 // 64-B writes pays for them at DRAM read/write turnarounds while the same writes issued as a burst with
@@ -1001,7 +981,7 @@ __device__ __forceinline__ void store_rec_verd(const EchoArgs& a, uint32_t t, ui
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0, int EARLY = 0>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE>& sm) {
     static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
@@ -1232,7 +1212,6 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
             } while (0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();  // meta/sums are rewritten by the next tile
-            if (EARLY) store_rec_verd<SUBT, WT>(a, r0 + (uint32_t)i * kWaves6 + wave, t_end, rec_o, verd_o, lane);
             rec[i] = rec_o;
             verd[i] = verd_o;
             alo[i] = alo_o;
@@ -1281,7 +1260,19 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     }
                 }
             }
-            if (!EARLY) store_rec_verd<SUBT, WT>(a, t, t_end, rec[i], verd[i], lane);
+            const uint32_t fi = t * (SUBT ? a.tile_live : (uint32_t)kTile) + lane;
+            if ((!SUBT || lane < a.tile_live) && fi < a.n) {
+                if (a.recs) {
+                    if (WT)
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            rec[i],
+                            __builtin_amdgcn_make_buffer_rsrc((void*)((u32x4*)a.recs + (uint64_t)uniform(t) * (SUBT ? a.tile_live : (uint32_t)kTile)),
+                                                              (short)0, -1, kRsrcFlags),
+                            (int)(lane * 16u), 0, kAuxSC1);
+                    else ((u32x4*)a.recs)[fi] = rec[i];
+                }
+                if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[i];
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();  // LDS rows are rewritten by the next round
@@ -1295,7 +1286,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack, int RS = 1, int LASTW = 0, int EARLY = 0>
+          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack, int RS = 1, int LASTW = 0>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW, WIRE> sm;
@@ -1304,7 +1295,7 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
     echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
-               SLACK, RS, LASTW, EARLY>(a, t_begin, t_end, sm);
+               SLACK, RS, LASTW>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
