@@ -196,7 +196,12 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     if (zerocopy(c)) {
         TRY(hipHostGetDevicePointer((void**)&c->d_umem, umem, 0));
     } else {
-        TRY(hipHostGetDevicePointer((void**)&c->m_umem, umem, 0));
+        /* the gather kernel's source; a runtime that gives no device alias on this device (a portable registration
+         * made on another one) leaves STAGED with its DMA copies: scattered chunks then copy their span */
+        if (hipHostGetDevicePointer((void**)&c->m_umem, umem, 0) != hipSuccess) {
+            c->m_umem = NULL;
+            (void)hipGetLastError();
+        }
         TRY(hipMalloc((void**)&c->d_umem, umem_size));
         TRY(hipMalloc((void**)&c->d_pack, (size_t)max_batch * PACK));
         TRY(hipHostMalloc((void**)&c->h_pack, (size_t)max_batch * PACK, hipHostMallocDefault));
@@ -321,7 +326,7 @@ static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const struct x
     /* an RX-loop-sized batch takes the gather kernel whatever its layout: one launch beats a DMA submission there
      * (64 x 64 B: 55.7 us per call vs 66.1 with the 2-D copy; 1024 x 1500 B: 126.2 vs 129.0 --
      * profiles/r04/pass1/hostlat_*.jsonl) */
-    const int small = n <= XSK_GPU_LOWLAT_MAX;
+    const int small = n <= XSK_GPU_LOWLAT_MAX && c->m_umem;
     if (!small && s && width <= s && (uint64_t)n * width <= budget && base + (uint64_t)(n - 1) * s + width <= c->umem_size) {
         if (hipMemcpy2DAsync(c->d_umem + base, s, c->umem + base, s, width, n, hipMemcpyHostToDevice, st) != hipSuccess)
             return -EIO;
@@ -329,7 +334,7 @@ static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const struct x
         c->staged[1]++;
         return 0;
     }
-    if (!small && hi - lo <= budget) {
+    if (!small && (hi - lo <= budget || !c->m_umem)) { /* (no mapped alias: the span, ordered after the previous pack) */
         if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, st) != hipSuccess) return -EIO;
         c->staged[0] += hi - lo;
         c->staged[2]++;
