@@ -15,13 +15,13 @@ import xsknet_amd as X  # noqa: E402
 
 # 0 as shipped (reference), 2 wire mode as shipped, 3 / 4 ranked streams with 4 / 8 row-loads per batch, 5 / 6 no SPLIT
 # (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4, 14 / 15 / 16 lean ranked streams (RS 2) with
-# 6 / 8 / 4 row-loads per batch, 17 / 18 no write-phase wait in the last round (reference / wire)
-VARIANTS = [0, 2, 3, 4, 5, 6, 7, 8, 9, 13, 14, 15, 16, 17, 18]
-WIRE_VARIANTS = (2, 6, 8, 18)
+# 6 / 8 / 4 row-loads per batch, 17 / 18 no write-phase wait in the last round (reference / wire), 21 wire mode on 128-B
+# windows (the wire kernel of rounds 1-4), 22 / 23 wire as shipped with VLAN only / SLACK 0
+VARIANTS = [0, 2, 3, 4, 5, 6, 7, 8, 9, 13, 14, 15, 16, 17, 18, 21, 22, 23]
+WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 18: X.OPT_ALL, 21: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL}
 
 
-@pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("grid", [0, 3])
+@pytest.mark.parametrize("variant,grid", [(v, 0) for v in VARIANTS] + [(v, 3) for v in (0, 2, 21)])
 def test_product_switch_variants(variant, grid):
     """The product kernel's source at alternative switch values (tune/xsk_tune_product.hip, the A/B candidates of
     tools/abbench.py's 1000 + v) on ragged mixed traffic at odd starts, shares of many rounds: every byte, verdict,
@@ -31,7 +31,7 @@ def test_product_switch_variants(variant, grid):
     from tests.test_gpu_parity import _shifted_mixed_batch
     umem, descs = _shifted_mixed_batch(9000, 2048 + 16, 1500, 0x5EED3232 + variant)
     ref = umem.copy()
-    opts = X.OPT_ALL if variant in WIRE_VARIANTS else 0
+    opts = WIRE_OPTS.get(variant, 0)
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
     d_umem, d_descs = to_dev(umem), to_dev(descs)
     n = len(descs)
@@ -50,7 +50,7 @@ def test_product_switch_variants(variant, grid):
     assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
 
 
-@pytest.mark.parametrize("variant", [5, 6])
+@pytest.mark.parametrize("variant", [5, 21])
 @pytest.mark.parametrize("flen", [42, 769, 1500, 4000])
 def test_product_switch_uniform_tiles(variant, flen):
     """The product kernel's switches on tiles whose frames share one length and one 16-B offset (the uniform
@@ -60,7 +60,7 @@ def test_product_switch_uniform_tiles(variant, flen):
     dev = _dev()
     n = 64 * 20 + 17  # past XSK_GPU_LOWLAT_MAX: the round kernel's geometry
     stride = ((flen + 16 + 255) // 256) * 256 + 256
-    opts = X.OPT_ALL if variant in (6, 8) else 0
+    opts = WIRE_OPTS.get(variant, 0)
     for off in (0, 1, 6, 15):
         umem = np.zeros(n * stride + 256, np.uint8)
         descs = oracle.synth_batch(umem, n, 256 + off, stride, seed=0x5EED2121 + flen + off, mode=0, len_lo=flen,
@@ -82,3 +82,54 @@ def test_product_switch_uniform_tiles(variant, flen):
             assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all(), (off, grid)
             assert (d_umem.cpu().numpy() == ref).all(), (off, grid)
             d_umem.copy_(to_dev(umem))
+
+
+@pytest.mark.parametrize("variant", [2, 21, 22, 23])
+def test_product_wire_variants_on_wire_traffic(variant):
+    """The wire-mode variants on the wire generator's traffic (tests/wire_frames.py: VLAN stacks, IHL 3-15 with
+    options -- headers reaching past a 64-B window --, fragments, tot_len errors, padding, bad checksums,
+    truncations) at all 16 start offsets, and on the golden frames: bit-exact vs the oracle with the variant's
+    options."""
+    import json
+    import os
+    from tests.conftest import ROOT
+    from tests.wire_frames import mixed_batch
+    L = X.tune_lib()
+    dev = _dev()
+    opts = WIRE_OPTS[variant]
+    umem, descs = mixed_batch(3000, 2048, seed=0x5EED4141 + variant, offsets=True)
+    cases = json.load(open(os.path.join(ROOT, "tests", "golden", "wire.json")))
+    g = len(cases) * 16
+    gu = np.zeros(g * 2048, np.uint8)
+    gd = np.zeros(g, descs.dtype)
+    for i in range(g):
+        fr = np.frombuffer(bytes.fromhex(cases[i // 16]["frame"]), np.uint8)
+        a = i * 2048 + (i % 16)
+        gu[a:a + len(fr)] = fr
+        gd[i] = (a, cases[i // 16]["len"], 0)
+    gd["addr"] += umem.size
+    umem = np.concatenate([umem, gu])
+    descs = np.ascontiguousarray(np.concatenate([descs, gd]), X.DESC_DTYPE)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
+    n = len(descs)
+    d_umem, d_descs = to_dev(umem), to_dev(descs)
+    d_verd = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
+    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
+    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
+    rc = L.xsk_gpu__product_variant(variant, 0, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
+                                    d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    v = d_verd.cpu().numpy()
+    bad = np.nonzero(v != v_ref)[0]
+    assert len(bad) == 0, (bad[:5], v[bad[:5]], v_ref[bad[:5]])
+    r = d_recs.cpu().numpy().view(X.REC_DTYPE)
+    bad = np.nonzero(r != r_ref)[0]
+    assert len(bad) == 0, (bad[:3], r[bad[:3]], r_ref[bad[:3]])
+    out = d_umem.cpu().numpy()
+    diff = np.nonzero(out != ref)[0]
+    assert len(diff) == 0, f"{len(diff)} bytes differ, first at {diff[:8]}"
+    part = ws[:1 << 15].cpu().numpy().view(np.uint64).reshape(-1, 4).sum(axis=0)
+    assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]

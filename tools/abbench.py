@@ -9,6 +9,7 @@ Variant -1 is the shipped entry point (xsk_gpu_echo_dev); v >= 0 is the product 
 switch v of tune/xsk_tune_product.hip (xsk_gpu__product_variant; 1000 + v is accepted too, the round-3 numbering).
 
     python tools/abbench.py --config c4 --variants=-1,9 --rounds 8
+    python tools/abbench.py --config c3 --opts 7 --variants=-1,2,21   # wire mode: -1 is xsk_gpu_echo_dev_opts(7)
 """
 import argparse
 import json
@@ -33,6 +34,9 @@ def main():
     ap.add_argument("--burst", type=int, default=0,
                     help="sustained regime: each variant runs BURST consecutive launches per round (the bench's back-"
                          "to-back loop) and only the second half of each burst is counted; 0 = interleave per launch")
+    ap.add_argument("--opts", type=int, default=0,
+                    help="wire-format options of the shipped entry point (-1; xsk_gpu_echo_dev_opts) -- the tuning "
+                         "variants carry their own (tune/xsk_tune_product.hip), so pair them accordingly")
     args = ap.parse_args()
     V = [int(v) for v in args.variants.split(",")]
     dev = torch.device("cuda", 0)
@@ -58,7 +62,7 @@ def main():
     def launch(v, b):
         u = slab[b * bb:(b + 1) * bb]
         if v < 0:
-            X.echo_dev(u, descs[b], n, verd, recs, stats, ws, stream)
+            X.echo_dev(u, descs[b], n, verd, recs, stats, ws, stream, opts=args.opts)
         else:
             rc = tune.xsk_gpu__product_variant(v % 1000, 0, u.data_ptr(), u.numel(), descs[b].data_ptr(), n,
                                                verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
@@ -101,25 +105,30 @@ def main():
     # every variant's outputs against the shipped entry point's on one fresh batch: slab, verdicts, records (a variant
     # that skips a store would otherwise time faster and pass unnoticed)
     regen()
-    ref_u = slab[:bb].clone()
-    ref_v = torch.full((n,), 0xEE, dtype=torch.uint8, device=dev)
-    ref_r = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    X.echo_dev(ref_u, descs[0], n, ref_v, ref_r, stats, ws, stream)
+    # a batch too large for a third copy (c5's 128 GiB) is verified on its first n / 16 frames (descriptors in
+    # address order, so they lie in the slab's first nv * stride bytes)
+    nv = n if torch.cuda.mem_get_info(dev)[0] > bb + (1 << 30) else n // 16
+    vb = nv * stride if nv < n else bb
+    ref_u = slab[:vb].clone()
+    ref_v = torch.full((nv,), 0xEE, dtype=torch.uint8, device=dev)
+    ref_r = torch.zeros(nv * 16, dtype=torch.uint8, device=dev)
+    X.echo_dev(ref_u, descs[0], nv, ref_v, ref_r, stats, ws, stream, opts=args.opts)
     verified = {}
     for v in V:
-        u = slab[bb:2 * bb] if pool > 1 else slab[:bb]
-        u.copy_(slab[:bb] if pool > 1 else ref_u)  # (pool of one: compare the shipped kernel with itself)
+        u = slab[bb:bb + vb] if pool > 1 else slab[:vb]
+        u.copy_(slab[:vb] if pool > 1 else ref_u)  # (pool of one: compare the shipped kernel with itself)
         verd.fill_(0xEE)
         recs.zero_()
         if v < 0:
-            X.echo_dev(u, descs[0], n, verd, recs, stats, ws, stream)
+            X.echo_dev(u, descs[0], nv, verd, recs, stats, ws, stream, opts=args.opts)
         else:
-            rc = tune.xsk_gpu__product_variant(v % 1000, 0, u.data_ptr(), u.numel(), descs[0].data_ptr(), n,
+            rc = tune.xsk_gpu__product_variant(v % 1000, 0, u.data_ptr(), u.numel(), descs[0].data_ptr(), nv,
                                                verd.data_ptr(), recs.data_ptr(), ws.data_ptr(), stream.cuda_stream)
             assert rc == 0, rc
         torch.cuda.synchronize()
-        verified[str(v)] = bool(torch.equal(u, ref_u) and torch.equal(verd, ref_v) and torch.equal(recs, ref_r))
-    out = {"config": args.config, "pool": pool, "rounds": args.rounds, "desc": desc, "outputs_equal_shipped": verified}
+        verified[str(v)] = bool(torch.equal(u, ref_u) and torch.equal(verd[:nv], ref_v) and
+                                torch.equal(recs[:nv * 16], ref_r))
+    out = {"config": args.config, "opts": args.opts, "pool": pool, "verified_frames": nv, "rounds": args.rounds, "desc": desc, "outputs_equal_shipped": verified}
     for v in V:
         t = np.sort(np.array(times[v]))
         k = len(t) // 8

@@ -207,7 +207,7 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
         echo_round_kernel<false, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else if (opts == 0)  // rounds of sub-tiles, writes as soon as a wave has read
         echo_round_kernel<false, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    else if (!small)  // wire mode: 128-B windows, one tile per wave per round
+    else if (!small)  // wire mode: the reference mode's 64-B windows and rounds, wire_header_phase64
         echo_round_kernel<true, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
     else
         echo_round_kernel<true, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);

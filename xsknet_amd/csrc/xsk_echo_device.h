@@ -836,6 +836,166 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
     return wb;
 }
 
+// Wire-format header phase on the reference-form stream (WW 64): the frame's 16-B aligned 64-B window in LDS
+// (`row`, frame byte i at row[off + i] while off + i < 64; bytes past it -- an ICMP header behind two VLAN tags and
+// IPv4 options -- are read from the UMEM) and the stream's ICMP sum of row bytes [off + 34, off + len), i.e. of the
+// message of a PLAIN frame (no tag, IHL 5, no Ethernet padding under STRICT).  Same spec, verdicts, records and
+// rewrite as wire_header_phase; a plain frame's sums come from the window and the stream exactly as in reference
+// mode, any other frame's from a re-read of its header and message bytes (rare traffic, per lane).
+__device__ __forceinline__ uint64_t sum_row_range(const uint8_t* rb, uint32_t lo, uint32_t hi) {
+    uint64_t acc = 0;  // LE dwords of the 16-B aligned row at rb, bytes [lo, hi) (absolute-alignment domain)
+    for (uint32_t o = lo & ~3u; o < hi; o += 4u) acc += keep_bytes(*(const uint32_t*)(rb + o), (int)o, (int)lo, (int)hi);
+    return acc;
+}
+
+__device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* row, uint32_t ic_raw, uint64_t addr,
+                                                    uint32_t len, bool ok, bool live, uint32_t wend, Counters& cnt,
+                                                    u32x4* rec_out, uint32_t* verd_out) {
+    const bool strict = (a.opts & XSK_GPU_OPT_STRICT_IPV4) != 0u;
+    const bool vlan = (a.opts & XSK_GPU_OPT_VLAN) != 0u;
+    const bool verify = (a.opts & XSK_GPU_OPT_VERIFY_CSUM) != 0u;
+    const uint32_t off = (uint32_t)addr & 15u;
+    uint8_t* p = row + off;
+    const uint8_t* g = a.umem + addr;
+    // frame byte i (i < len, so inside the UMEM): the window, or memory behind it
+    auto fb = [&](uint32_t i) -> uint32_t { return off + i < (uint32_t)kWin ? (uint32_t)p[i] : (uint32_t)g[i]; };
+    auto be16 = [&](uint32_t i) -> uint32_t { return (fb(i) << 8) | fb(i + 1); };
+    uint32_t verdict = XSK_GPU_TX_REPLY;
+    uint32_t l3 = 14, hl = 20, end = len, et = 0, tags = 0;
+    bool hdrs = false;
+    if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
+    else if (len < 14) verdict = XSK_GPU_DROP_SHORT;
+    else {
+        et = be16(12);
+        bool cut = false;
+        if (vlan) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (!cut && (et == 0x8100u || et == 0x88A8u) && tags == (uint32_t)t) {
+                    if (len < l3 + 4) cut = true;
+                    else {
+                        et = be16(l3 + 2);
+                        l3 += 4;
+                        tags++;
+                    }
+                }
+            }
+        }
+        if (cut) verdict = XSK_GPU_DROP_SHORT;
+        else if (et != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;
+        else if (len < l3 + 20) verdict = XSK_GPU_DROP_SHORT;
+        else {
+            bool bad = false;
+            if (strict) {
+                const uint32_t vihl = fb(l3);
+                if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
+                else {
+                    hl = 4u * (vihl & 15u);
+                    const uint32_t tot = be16(l3 + 2);
+                    if (tot < hl + 8 || l3 + tot > len) bad = true;
+                    else if (be16(l3 + 6) & 0x3FFFu) bad = true;
+                    else end = l3 + tot;
+                }
+            }
+            if (bad) verdict = XSK_GPU_DROP_BAD_IP;
+            else if (fb(l3 + 9) != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
+            else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
+            else hdrs = true;
+        }
+    }
+    const uint32_t l4 = l3 + hl;
+    uint32_t ip_sum = 0, ic_sum = 0, itype = 0, icode = 0, csum_in = 0, flags = 0;
+    if (hdrs) {
+        if (l3 == 14u && l4 == 34u && end == len) {
+            // plain: the IPv4 header [14, 34) from the window (frame-relative dwords, as header_phase_ref) and the
+            // message [34, len) from the stream
+            const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+            uint32_t h[9];
+#pragma unroll
+            for (int k = 3; k < 9; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+            uint32_t acc = dot2_halves(h[3] >> 16, dot2_halves(h[4], dot2_halves(h[5], 0u)));
+            acc = dot2_halves(h[8] & 0xFFFFu, dot2_halves(h[7], dot2_halves(h[6], acc)));
+            ip_sum = bswap16(fold32(acc));
+            ic_sum = fold32(ic_raw);
+            if (!((uint32_t)addr & 1u)) ic_sum = bswap16(ic_sum);
+        } else {  // tags, options or padding: re-read the header and the message (absolute-alignment domain)
+            const uint8_t* rb = a.umem + (addr & ~15ull);
+            ip_sum = fold64(sum_row_range(rb, off + l3, off + l4));
+            ic_sum = fold64(sum_row_range(rb, off + l4, off + end));
+            if (!((uint32_t)addr & 1u)) {
+                ip_sum = bswap16(ip_sum);
+                ic_sum = bswap16(ic_sum);
+            }
+        }
+        itype = fb(l4);
+        icode = fb(l4 + 1);
+        csum_in = be16(l4 + 2);
+        if (ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
+        if (ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
+        if (tags) flags |= XSK_GPU_F_VLAN;
+        if (hl > 20u) flags |= XSK_GPU_F_IP_OPTIONS;
+        if (itype != 8u || (strict && icode != 0u)) verdict = XSK_GPU_DROP_NOT_ECHO;
+        else if (verify && (ip_sum != 0xFFFFu || ic_sum != 0xFFFFu)) verdict = XSK_GPU_DROP_BAD_CSUM;
+    }
+    const bool tx = hdrs && verdict == XSK_GPU_TX_REPLY;
+    const uint32_t vihl = hdrs ? fb(l3) : 0u, proto = hdrs ? 1u : 0u;
+    uint32_t csum_out = csum_in;
+    bool wb = false;
+    if (tx) {
+        // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY) on the LE-loaded field (xsk_receive.c:101-111)
+        const uint32_t csum_le = ((csum_in & 0xFFu) << 8) | (csum_in >> 8);
+        uint32_t c16 = (~csum_le) & 0xFFFFu;
+        c16 = (c16 + 0xFFF7u) & 0xFFFFu;
+        c16 += c16 < 0xFFF7u ? 1u : 0u;
+        const uint32_t csum_new_le = (~c16) & 0xFFFFu;
+        csum_out = bswap16(csum_new_le);
+        // xsk_receive.c:148-157 at the parsed offsets: MACs and addresses lie in the window (off + l3 + 20 <= 57)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const uint8_t x = p[i];
+            p[i] = p[6 + i];
+            p[6 + i] = x;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint8_t x = p[l3 + 12 + i];
+            p[l3 + 12 + i] = p[l3 + 16 + i];
+            p[l3 + 16 + i] = x;
+        }
+        if (off == 0u && l4 + 4u <= (uint32_t)kWin && wend >= (uint32_t)kWin) {
+            p[l4] = 0;  // whole 64-B sector, stored in the write phase
+            p[l4 + 2] = (uint8_t)csum_new_le;
+            p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+            wb = true;
+        } else {  // byte-exact: only the rewritten bytes
+            uint8_t* pkt = a.umem + addr;
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pkt[i] = p[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
+            pkt[l4] = 0;
+            pkt[l4 + 2] = (uint8_t)csum_new_le;
+            pkt[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+        }
+    }
+    u32x4 r;
+    r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
+    r.y = icode | (vihl << 8) | ((hdrs ? et : 0u) << 16);
+    r.z = csum_in | (csum_out << 16);
+    r.w = ip_sum | (ic_sum << 16);
+    *rec_out = r;
+    *verd_out = verdict;
+    if (live) {
+        cnt.rxp += 1;
+        cnt.rxb += len;
+        if (tx) {
+            cnt.txp += 1;
+            cnt.txb += len;
+        }
+    }
+    return wb;
+}
+
 // LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB in reference mode): TPW header-window
 // tiles per wave, the per-frame metadata and sums, the ranked streams' sort rows, the counter rows.
 template <int TPW, bool WIRE>
@@ -965,12 +1125,14 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // echo6_body: the work over the tiles [t_begin, t_end) of one workgroup (every wave of the workgroup calls
 // it with the same range); echo_round_kernel runs it once per workgroup on its static share, the
 // low-latency resident kernel (xsk_lowlat.hip) once per doorbell.
-//   TPW   tiles per wave per round (reference mode 2; wire mode, whose windows are 128 B, and sub-tiles 1)
+//   TPW   tiles per wave per round (2; wire mode on 128-B windows and sub-tiles 1)
 //   SYNC  how a wave enters its write phase.  0: at once (one-round small batches); 2: a wave at least half
 //         of whose frames this round have >= HEAVY bytes waits until every wave of the workgroup but SLACK has
 //         read the round (LDS arrival counter), lighter waves go ahead -- the phase separation pays where reads
 //         dominate, and costs latency hiding where frames are short
-//   WIRE  the wire-format mode (a.opts != 0): 128-B windows, wire_header_phase
+//   WIRE  the wire-format mode (a.opts != 0): on 64-B windows (WW, the launched kernel) the reference mode's streams
+//         and rounds with wire_header_phase64; on 128-B windows (sub-tiles, the low-latency kernel) wire-form streams
+//         and wire_header_phase
 //   SUBT  tiles of a.tile_live frames (small batches: the batch spreads over every wave)
 //   TRACE wave 0 stamps the body's phase boundaries into a.trace (the low-latency kernel's diagnostics)
 //   DLDS  the descriptors may already be in the LDS (a.desc_in_lds, the low-latency kernel's first poll)
@@ -981,16 +1143,20 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0, int WW = kWireWin>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
-                                           Echo6Smem<TPW, WIRE>& sm) {
-    static_assert(!WIRE || TPW == 1, "wire windows are 128 B: one tile per wave per round");
+                                           Echo6Smem<TPW, WIRE && WW != kWin>& sm) {
+    // WW: wire mode's LDS window -- 128 B (the whole parsed header in LDS, the stream summing bytes from 128 on, one
+    // tile per wave per round) or 64 B (reference-form streams and rounds, wire_header_phase64)
+    constexpr bool SW = WIRE && WW != kWin;  // wire-form streams: 128-B rows, the stream's ICMP part from byte 128
+    static_assert(!SW || TPW == 1, "wire windows of 128 B: one tile per wave per round");
+    static_assert(WW == kWin || WW == kWireWin, "wire window: 64 or 128 B");
     static_assert(SYNC == 0 || SYNC == 2, "write phases: at once (0) or heavy waves wait for the round (2)");
     static_assert(SLACK >= 0 && SLACK < kWaves6, "SLACK: waves a heavy wave does not wait for");
     constexpr int U = kU;
-    constexpr bool REF = !WIRE;                          // reference-mode stream choices (D2 / MID / SKM)
-    constexpr bool PAIR = REF && TPW == 2 && !SUBT;      // paired short tiles
-    constexpr uint32_t kRowW = WIRE ? (uint32_t)kWireWin : (uint32_t)kWin;  // LDS row (header window) bytes
+    constexpr bool REF = !SW;                            // reference-form stream choices (D2 / MID / SKM)
+    constexpr bool PAIR = !WIRE && TPW == 2 && !SUBT;    // paired short tiles (header_phase_ref)
+    constexpr uint32_t kRowW = SW ? (uint32_t)kWireWin : (uint32_t)kWin;  // LDS row (header window) bytes
     auto& s_hdr = sm.hdr;
     uint32_t& s_arrive = sm.arrive;
     if (SYNC == 2) {
@@ -1088,7 +1254,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     WinLoader ld;
                     ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
                                                              fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
-                    if (WIRE && short_tile) {
+                    if (SW && short_tile) {
                         // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
                         // nothing lies past byte 128, so the streamed part of every sum is zero
                         const uint32_t kk = lane & 7u, ro = 16u * kk;
@@ -1164,11 +1330,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                         if (RS == 2 && REF && fast && uniform(max_nit_lane(nit)) <= 257u)
                             stream_tile_ranked2<UR, PRIO>(ld.r, meta, sm.sort[wave], rows, sums_ic, nit,
                                                           nit ? (uint32_t)(a16 - wlo) : 0u, rowhi, lim, off, lane);
-                        else if (fast) stream_tile_sorted<UR, true, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
-                        else stream_tile_sorted<UR, false, WIRE, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        else if (fast) stream_tile_sorted<UR, true, SW, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<UR, false, SW, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
-                        stream_tile_uniform<U, WIRE, USPLIT, PRIO>(ld.r, meta, rows, sums_ic, uniform(nit),
-                                                     WIRE ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
+                        stream_tile_uniform<U, SW, USPLIT, PRIO>(ld.r, meta, rows, sums_ic, uniform(nit),
+                                                     SW ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
                     } else {
                         // every frame the same number of row-loads, but different offsets or ends: per-step streams
                         for (uint32_t s = 0; s < 16; ++s) {
@@ -1184,11 +1350,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                             RowSums rs;
                             if (fast) {
                                 ld.rel = fm.rel;
-                                stream_frame<U, WinLoader, WIRE, REF>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                                stream_frame<U, WinLoader, SW, REF>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                             } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
                                 FarLoader fl;
                                 fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
-                                stream_frame<U, FarLoader, WIRE, REF>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                                stream_frame<U, FarLoader, SW, REF>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                             }
                             const uint32_t ric = row_sum_dpp(fold64(rs.ic));
                             if (k == 15u) sums_ic[f] = ric;
@@ -1202,9 +1368,12 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
                 bool wb;
-                if (WIRE)
+                if (WIRE && SW)
                     wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
                                            &verd_o);
+                else if (WIRE)
+                    wb = wire_header_phase64(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
+                                             &verd_o);
                 else
                     wb = header_phase_ref(a, rows + lane * kWin, ic_raw, addr, len, in_n, ok, parse, cnt, &rec_o,
                                           &verd_o);
@@ -1284,18 +1453,21 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
-// a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).
+// a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).  Large wire batches run on 64-B windows
+// (round 5: 44 / 282 / 186 us for c2 / c3 / c4 against 71 / 298 / 220 on the 128-B windows of rounds 1-4,
+// profiles/r05/).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = (WIRE || SUBT) ? 0 : kRefSlack, int RS = 1, int LASTW = 0>
+          int SLACK = SUBT ? 0 : kRefSlack, int RS = 1, int LASTW = 0, int WW = (WIRE && !SUBT) ? kWin : kWireWin>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
-    constexpr int TPW = (WIRE || SUBT) ? 1 : kRefTPW;
-    __shared__ Echo6Smem<TPW, WIRE> sm;
+    constexpr bool SW = WIRE && WW != kWin;  // wire mode on 128-B windows
+    constexpr int TPW = (SW || SUBT) ? 1 : kRefTPW;
+    __shared__ Echo6Smem<TPW, SW> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, WIRE ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
-               SLACK, RS, LASTW>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, SW ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
+               SLACK, RS, LASTW, WW>(a, t_begin, t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
