@@ -546,8 +546,8 @@ def main():
 
     if rank == 0:
         value = frames_all / wall_max / 1e6
-        traffic, traffic_src = (None, "none: wire mode is not profiled") if args.opts else \
-            traffic_from_profiles(args.config, kernel, X.build_id())
+        traffic, traffic_src = traffic_from_profiles(args.config + (f"_opts{args.opts}" if args.opts else ""), kernel,
+                                                     X.build_id())
         res = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -14,6 +14,8 @@ run bench_c4 200 python bench.py --config c4 --steps 20 --warmup 5 --no-cpu || e
 run bench_c2 200 python bench.py --config c2 --steps 20 --warmup 5 --no-cpu || exit 1
 run bench_p98 200 python bench.py --config p98 --steps 20 --warmup 5 --no-cpu || exit 1
 run bench_c3_wire 200 python bench.py --opts 7 --steps 20 --warmup 5 --no-cpu || exit 1
+run bench_c4_wire 200 python bench.py --config c4 --opts 7 --steps 20 --warmup 5 --no-cpu || exit 1
+run bench_c2_wire 200 python bench.py --config c2 --opts 7 --steps 20 --warmup 5 --no-cpu || exit 1
 run bench_c5 300 python bench.py --config c5 --steps 3 --warmup 1 --no-cpu || exit 1
 XSK_BENCH_SHARE_GPU=1 run bench_c3_n2_shared 200 python bench.py --gpus 2 --steps 10 --warmup 2 --pool-cap 8 --no-cpu || exit 1
 for c in c3 c4 c2; do

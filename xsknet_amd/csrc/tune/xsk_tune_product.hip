@@ -113,7 +113,7 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         case 17: echo_round_kernel<false, false, kUR, true, true, kRefSlack, 1, 1><<<gg, bb, 0, s>>>(args, per); break;
         case 18: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, kRefSlack, 1, 1><<<gg, bb, 0, s>>>(args, per); break;
         // 21: wire mode on 128-B windows (wire-form streams, one tile per wave per round, SLACK 0: the wire kernel of
-        // rounds 1-4, replaced by the 64-B windows of wire_header_phase64); 22: as shipped with no option bit but VLAN;
+        // rounds 1-4 until replaced by the 64-B windows of wire_header_phase64); 22: as shipped with no option bit but VLAN;
         // 23: as shipped with SLACK 0
         case 21: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0, 1, 0, kWireWin><<<gg, bb, 0, s>>>(args, per); break;
         case 22: args.opts = XSK_GPU_OPT_VLAN; echo_round_kernel<true, false><<<gg, bb, 0, s>>>(args, per); break;

@@ -1454,8 +1454,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
 // a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).  Large wire batches run on 64-B windows
-// (round 5: 44 / 282 / 186 us for c2 / c3 / c4 against 71 / 298 / 220 on the 128-B windows of rounds 1-4,
-// profiles/r05/).
+// (44 / 280 / 185 us for c2 / c3 / c4 against 71 / 298 / 215 on the 128-B windows of rounds 1-4, in-process A/B,
+// profiles/r04/wire64/).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
           int SLACK = SUBT ? 0 : kRefSlack, int RS = 1, int LASTW = 0, int WW = (WIRE && !SUBT) ? kWin : kWireWin>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
