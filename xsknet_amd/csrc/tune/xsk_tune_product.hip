@@ -92,10 +92,7 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
     switch (variant) {
         case 0: echo_round_kernel<false, false><<<gg, bb, 0, s>>>(args, per); break;
         case 2: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false><<<gg, bb, 0, s>>>(args, per); break;
-        // 3 / 4: ranked (ragged-tile) streams with 4 (round 2's) / 8 row-loads per batch instead of kUR = 6 (the
-        // uniform stream keeps kU = 4)
-        case 3: echo_round_kernel<false, false, 4><<<gg, bb, 0, s>>>(args, per); break;
-        case 4: echo_round_kernel<false, false, 8><<<gg, bb, 0, s>>>(args, per); break;
+        // (3 / 4, ranked streams with 4 / 8 row-loads per batch: measured against kUR = 6 in rounds 3-4 and removed)
         // 5 / 6: the uniform stream's row-loads in batches of 4 and a remainder (round 2's, no SPLIT), reference / wire
         case 5: echo_round_kernel<false, false, kUR, false><<<gg, bb, 0, s>>>(args, per); break;
         case 6: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, false><<<gg, bb, 0, s>>>(args, per); break;
