@@ -48,6 +48,8 @@
 //            contiguous, 4+2>, 63 <8, contiguous, 12>, 64 <16, contiguous, 12>; 65: 62 with the windows of
 //            every 2 tiles of a wave written after them (2 write phases per share, no sync); 66: 65 with a
 //            workgroup barrier before each write phase
+//   mode 70-73 (DEFER): 62's single end phase with the first half share's windows parked in a contiguous side buffer
+//            between (70 default stores, 71 nontemporal, 72 write-through, 73 = 70 without the end barrier)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -284,15 +286,30 @@ __global__ __launch_bounds__(NW * 64) void wexp_pers(const uint8_t* buf, uint32_
 // s + 1's 6 loads issued before step s is summed (12 in flight).
 template <int NW, bool FRONT, int LM, int ENDW = 0>
 __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
-                                                       unsigned long long* out) {
+                                                       unsigned long long* out, uint8_t* side = nullptr) {
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     const uint32_t q = lane >> 4, k = lane & 15u;
     const uint32_t ntiles = (n + 63) / 64;
     const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
     uint64_t acc = 0;
     for (uint32_t c = wave; c < per; c += NW) {
+        // ENDW 4-7 (DEFER): the windows of the share's first half ("round 0", c < 2 NW) go to a contiguous side
+        // buffer right after the tile (4 KiB per tile, coalesced); every window is scattered in one end phase
+        if (ENDW >= 4 && c >= 2u * NW && c < 4u * NW) {
+            const uint32_t tp = blockIdx.x * per + c - 2u * NW;  // the round-0 tile this wave read two tiles ago
+            const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
+            if (tp < ntiles) {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    u32x4* dst = (u32x4*)(side + (uint64_t)tp * 4096u + (uint32_t)rr * 1024u + lane * 16u);
+                    if (ENDW == 5) __builtin_nontemporal_store(w, dst);
+                    else if (ENDW == 6) __builtin_amdgcn_raw_buffer_store_b128(w, __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, 16, 0x00020000), 0, 0, 16);
+                    else *dst = w;
+                }
+            }
+        }
         const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
-        if (ENDW >= 2 && c >= 2u * NW && ((c / NW) & 1u) == 0u) {  // a write phase after every 2 tiles
+        if ((ENDW == 2 || ENDW == 3) && c >= 2u * NW && ((c / NW) & 1u) == 0u) {  // a write phase after every 2 tiles
             if (ENDW == 3) __syncthreads();
             const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
             for (uint32_t cc = c - 2u * NW; cc < c; cc += NW) {
@@ -349,15 +366,22 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
         }
     }
     if (ENDW) {  // every frame's 64-B window written once, after the workgroup has read its whole share
-        if (ENDW != 2) __syncthreads();
+        if (ENDW != 2 && ENDW != 7) __syncthreads();
         const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
-        for (uint32_t c = ENDW >= 2 ? wave + ((per - wave + NW - 1) / NW - 1) / 2 * 2 * NW : wave; c < per; c += NW) {
+        for (uint32_t c = (ENDW == 2 || ENDW == 3) ? wave + ((per - wave + NW - 1) / NW - 1) / 2 * 2 * NW : wave; c < per;
+             c += NW) {
             const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
             if (t >= ntiles) continue;
+            u32x4 ws[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                ws[r] = w;
+                if (ENDW >= 4 && c < 2u * NW) ws[r] = *(const u32x4*)(side + (uint64_t)t * 4096u + (uint32_t)r * 1024u + lane * 16u);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t f = t * 64u + (uint32_t)r * 16u + (lane >> 2);
-                if (f < n) *(u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u)) = w;
+                if (f < n) *(u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u)) = ws[r];
             }
         }
     }
@@ -423,6 +447,12 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 64: wexp_ladder<16, false, 2, 1><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 65: wexp_ladder<16, false, 1, 2><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 66: wexp_ladder<16, false, 1, 3><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        // 70-73 (DEFER): 62's single end phase, the first half share's windows parked in a contiguous side buffer
+        // between (70 default stores, 71 nontemporal, 72 sc1 write-through, 73 = 70 without the end barrier)
+        case 70: wexp_ladder<16, false, 1, 4><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
+        case 71: wexp_ladder<16, false, 1, 5><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
+        case 72: wexp_ladder<16, false, 1, 6><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
+        case 73: wexp_ladder<16, false, 1, 7><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
         case 13: wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         case 14: wexp_kernel<14><<<g, b, 0, s>>>(p, n, stride, len, o, side);
                  wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;

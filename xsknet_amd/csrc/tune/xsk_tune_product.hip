@@ -27,6 +27,10 @@
 // (round 3 measured BAL -- static shares for 15/16 .. 3/4 of the tiles, the rest a pool drained with claims on a
 // device counter in shrinking sub-tile units -- as variants 20-27 of commit a9c3d74: c3 +19 to +60 us, c4 +8 to +48,
 // c2 +11 to +30; profiles/r03/balance/.  Removed: it needed a counter-output switch in the product body.)
+// (round 4 measured DEFER -- rounds in pairs, the first parking its patched windows in a contiguous workspace scratch for
+// ONE scatter at the end of a two-round share: c3 286.4 vs 281.8 us, c4 191.8 vs 180.3, c2 46.6 vs 36.7; and the first
+// round's records and verdicts held in VGPRs until the second's write phase: c3 280.1 vs 278.8, c4 179.5 vs 179.3, c2
+// 34.9 vs 34.9, wire c3 286.1 vs 286.5; profiles/r04/defer/; removed)
 #include <errno.h>
 
 #include "../xsk_echo_device.h"
