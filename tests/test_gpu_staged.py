@@ -3,7 +3,8 @@
 The reference recycles frames through a LIFO free stack (src/lib/xsk_receive.c:55-71, :201-217, :226-227), so after the
 first wrap an RX batch's addresses are scrambled across the UMEM.  STAGED copies only the bytes the transform reads
 (xsk_gpu__read_span: a 2-D DMA copy for a uniform stride, one copy of a dense span, else the per-frame gather kernel
-across PCIe), and chunk i+1's copy-in waits for chunk i's header pack.  Every test here is byte-exact against the
+across PCIe); a chunk's copy-in that may write another chunk's mirror bytes (unaligned frames, the span copy) waits for
+the previous chunk's header pack, and the next chunk for its pack, while contained copy-ins run back to back.  Every test here is byte-exact against the
 oracle, and the copy-in record (xsk_gpu__staged_stats) bounds the bytes moved host->device."""
 import gc
 import time
@@ -17,9 +18,8 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import xsknet_amd as X  # noqa: E402
+from tests.staged_plan import CHUNK_FRAMES as CHUNK, stage_chunks  # noqa: E402
 from tests.test_gpu_host import COUNTERS, check, run_batches  # noqa: E402
-
-CHUNK = 32768  # CHUNK_FRAMES of xsk_gpu_host.c
 
 
 def _dev():
@@ -68,8 +68,31 @@ def test_staged_scrambled_multi_chunk():
     tot = {k: int(st[k]) for k in COUNTERS}
     check(umem, work, descs, v, r, tot)
     spans = sum(read_span(int(a), int(ln), umem.nbytes) for a, ln in zip(descs["addr"], descs["len"]))
-    assert rec["gather"] == 4 and rec["strided"] == 0 and rec["span"] == 0, rec
+    k = len(stage_chunks(n))  # 32 768, 32 768, then the halving tail: 7 chunks
+    assert rec["gather"] == k and rec["strided"] == 0 and rec["span"] == 0, rec
+    assert rec["contained"] == k, rec  # 16-B aligned frames: the copy-ins run without cross-chunk waits
     assert rec["h2d_bytes"] == spans <= 1.1 * owned_bytes(descs), (rec, spans, owned_bytes(descs))
+
+
+def test_staged_strided_multi_chunk_back_to_back():
+    """The host-inclusive bench's shape (1500-B frames at a 4 KiB stride, 16-B aligned) over 3 x 32 768 + 777 frames:
+    every chunk's 2-D copy-in is contained, so the copy-ins run back to back on the copy stream under the other
+    chunks' transforms and packs -- exact, three times."""
+    _dev()
+    n = 3 * CHUNK + 777
+    umem = np.zeros(n * 4096, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 4096, 0x5EED4C05, mode=1, len_lo=1500, len_hi=1500,
+                               threads=min(16, oracle.cpu_threads()))
+    for rep in range(3):
+        work = umem.copy()
+        with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
+            v, r, st = ctx.process(descs)
+            rec = ctx.staged_stats()
+        check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
+        # (a tail chunk of <= 1024 frames is RX-loop sized: the gather kernel)
+        ch = stage_chunks(n)
+        small = sum(m <= 1024 for m in ch)
+        assert rec["contained"] == len(ch) and rec["strided"] == len(ch) - small and rec["gather"] == small, (rec, ch)
 
 
 def packed(lens, seed):
@@ -108,7 +131,7 @@ def test_staged_multi_chunk_overlapping_spans():
             v, r, st = ctx.process(descs)
             rec = ctx.staged_stats()
         check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
-        assert rec["gather"] == 3, rec
+        assert rec["gather"] == len(stage_chunks(n)) and rec["contained"] == 0, rec
 
 
 def test_staged_copy_in_paths():

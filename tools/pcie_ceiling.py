@@ -49,6 +49,7 @@ def main():
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s0)
+            s1.wait_stream(s0)  # the second stream's chunks start after e0
             fn()
             s0.wait_stream(s1)
             e1.record(s0)

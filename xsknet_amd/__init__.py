@@ -298,10 +298,11 @@ class EchoContext:
 
     def staged_stats(self):
         """xsk_gpu__staged_stats of a STAGED context: bytes copied host->device since init, and the chunks copied as
-        one 2-D stride / one dense span / by the gather kernel."""
-        out = (C.c_uint64 * 4)()
+        one 2-D stride / one dense span / by the gather kernel, and the chunks whose copy-in wrote only their own frames'
+        mirror bytes (run without waiting for the previous chunk's header pack)."""
+        out = (C.c_uint64 * 5)()
         _check("xsk_gpu__staged_stats", lib().xsk_gpu__staged_stats(self._ctx, out))
-        return {"h2d_bytes": out[0], "strided": out[1], "span": out[2], "gather": out[3]}
+        return {"h2d_bytes": out[0], "strided": out[1], "span": out[2], "gather": out[3], "contained": out[4]}
 
     def lowlat_tune(self, tile_frames: int = 0, groups: int = 0, timeout_us: int = 0) -> None:
         """Tool / test knobs of a LOWLAT context (xsk_gpu__lowlat_tune): frames per wave, serving workgroups,

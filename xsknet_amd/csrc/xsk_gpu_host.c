@@ -18,10 +18,12 @@
  *             frames cover it densely, else -- AF_XDP's recycled, scattered descriptors -- a gather kernel that
  *             moves each frame's own bytes across PCIe), transformed in HBM, and only the 38 rewritten header
  *             bytes of TX_REPLY frames are copied back and scattered into the UMEM — bytes the batch does not own
- *             are never written.  Batches of more than one chunk run as a two-stream pipeline: chunk i+1's
- *             copy-in waits for chunk i's header pack (a frame's read span may reach into a neighbour's first
- *             bytes, which chunk i may just have rewritten in the mirror), its copy-back overlaps chunk i+1's
- *             copy-in, and the host scatters chunk i while later chunks are still in flight.
+ *             are never written.  Batches of more than one chunk run as a two-stream pipeline: the copy-ins of
+ *             16-B aligned frames by 2-D copy or gather write only their own frames' mirror bytes and run back
+ *             to back; any other copy-in (an unaligned frame's read span may reach into a neighbour's first bytes,
+ *             which another chunk may just have rewritten in the mirror) waits for the previous chunk's header
+ *             pack, and the chunk after it for its pack; a chunk's copy-back overlaps the next chunk's copy-in,
+ *             and the host scatters chunk i while later chunks are still in flight.
  */
 #define _GNU_SOURCE
 #define __HIP_PLATFORM_AMD__ 1
@@ -35,6 +37,8 @@
 
 #define NSTREAMS 2
 #define CHUNK_FRAMES 32768u /* staged pipeline granule: ~49 MB of 1500-B frames per copy-in */
+#define TAIL_FRAMES 4096u   /* staged: the last chunks halve down to this, so the work left after the last copy-in
+                             * (transform, pack, copy-back, host scatter of one chunk) is short */
 #define PACK 96u            /* staged: bytes per frame of the packed rewritten headers (wire mode <= 86) */
 #define WIRE_WIN 128u       /* wire mode's header window (xsk_wire.hip) */
 
@@ -64,7 +68,9 @@ struct xsk_gpu_ctx {
     hipStream_t stream[NSTREAMS];
     hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
     hipEvent_t* packed; /* STAGED [max_chunks]: chunk's rewritten headers are packed (its mirror bytes are free) */
-    uint64_t staged[4]; /* STAGED: bytes copied in, chunks copied as 2-D strides / dense spans / by the gather kernel */
+    hipEvent_t* in_done; /* STAGED [max_chunks]: chunk's copy-in has landed in the mirror */
+    uint64_t staged[5]; /* STAGED: bytes copied in, chunks copied as 2-D strides / dense spans / by the gather kernel,
+                         * chunks whose copy-in was contained (not ordered after the previous chunk's pack) */
     int registered;   /* this context registered the UMEM (and unregisters it at fini) */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
@@ -118,6 +124,19 @@ static void ll_slot_give(int device) {
     if (device >= 0 && device < LL_MAX_DEV) atomic_fetch_sub(&g_ll_slots[device], 1);
 }
 
+/* STAGED: frames in the next chunk of an n-frame batch with `rem` frames left -- a batch of at most CHUNK_FRAMES is
+ * one chunk; a larger one takes CHUNK_FRAMES while two or more chunks' worth remain, then halves (multiples of 16)
+ * down to TAIL_FRAMES. */
+static uint32_t stage_chunk(uint32_t n, uint32_t rem) {
+    if (n <= CHUNK_FRAMES || rem <= TAIL_FRAMES) return rem;
+    if (rem >= 2u * CHUNK_FRAMES) return CHUNK_FRAMES;
+    const uint32_t half = ((rem / 2u) + 15u) & ~15u;
+    return half < TAIL_FRAMES ? TAIL_FRAMES : half;
+}
+/* an upper bound of the chunks of any batch of at most n frames (the halving tail adds at most 5; checked by
+ * tests/test_staged_plan.py's restatement) */
+static uint32_t stage_chunks_max(uint32_t n) { return (n + CHUNK_FRAMES - 1) / CHUNK_FRAMES + 5u; }
+
 /* ZEROCOPY and LOWLAT read the UMEM in place through its mapped alias */
 static int zerocopy(const xsk_gpu_ctx* c) { return c->mode != XSK_GPU_MODE_STAGED; }
 
@@ -160,6 +179,11 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
             if (c->packed[i]) (void)hipEventDestroy(c->packed[i]);
         free(c->packed);
     }
+    if (c->in_done) {
+        for (uint32_t i = 0; i < c->max_chunks; i++)
+            if (c->in_done[i]) (void)hipEventDestroy(c->in_done[i]);
+        free(c->in_done);
+    }
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamDestroy(c->stream[s]);
     free(c);
@@ -186,7 +210,7 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     c->umem = (uint8_t*)umem;
     c->umem_size = umem_size;
     c->max_batch = max_batch;
-    c->max_chunks = mode == XSK_GPU_MODE_STAGED ? (max_batch + CHUNK_FRAMES - 1) / CHUNK_FRAMES : 1;
+    c->max_chunks = mode == XSK_GPU_MODE_STAGED ? stage_chunks_max(max_batch) : 1;
     TRY(hipSetDevice(device));
     for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamCreateWithFlags(&c->stream[s], hipStreamNonBlocking));
     if (!prereg) { /* mapped in every mode: STAGED's gather kernel reads scattered frames through the alias */
@@ -239,8 +263,15 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
             rc = -ENOMEM;
             goto out;
         }
-        for (uint32_t i = 0; i < c->max_chunks; i++)
+        c->in_done = (hipEvent_t*)calloc(c->max_chunks, sizeof(hipEvent_t));
+        if (!c->in_done) {
+            rc = -ENOMEM;
+            goto out;
+        }
+        for (uint32_t i = 0; i < c->max_chunks; i++) {
             TRY(hipEventCreateWithFlags(&c->packed[i], hipEventDisableTiming));
+            TRY(hipEventCreateWithFlags(&c->in_done[i], hipEventDisableTiming));
+        }
     }
     if (c->mode == XSK_GPU_MODE_LOWLAT) {
         rc = xsk_gpu__lowlat_start(&c->ll, c->d_umem, umem_size, 0);
@@ -269,9 +300,9 @@ void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* c) {
     xsk_gpu__lowlat_stop(c->ll);
 }
 
-int xsk_gpu__staged_stats(const xsk_gpu_ctx* c, uint64_t out[4]) {
+int xsk_gpu__staged_stats(const xsk_gpu_ctx* c, uint64_t out[5]) {
     if (!c || !out || c->mode != XSK_GPU_MODE_STAGED) return -EINVAL;
-    for (int i = 0; i < 4; i++) out[i] = c->staged[i];
+    for (int i = 0; i < 5; i++) out[i] = c->staged[i];
     return 0;
 }
 int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
@@ -299,61 +330,91 @@ int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     return 0;
 }
 
-/* Copy-in of the bytes the transform reads for frames d[0..n) (xsk_gpu__read_span) into the device mirror, on stream st:
+/* Copy-in of the bytes the transform reads for frames d[0..n) (xsk_gpu__read_span) into the device mirror:
  *   - n <= XSK_GPU_LOWLAT_MAX (an RX-loop batch): the gather kernel below, whatever the layout;
  *   - a uniform frame stride whose strided rows carry at most 10 % more than those bytes: one 2-D DMA copy;
  *   - frames covering their span [lo, hi) densely (at most 10 % of it between frames): one DMA copy of the span;
  *   - otherwise -- AF_XDP's recycled descriptors scatter over the UMEM (xsk_receive.c:55-71, :201-217, :226-227) --
  *     the gather kernel moves each frame's own bytes across PCIe (dd: the chunk's descriptors, already on the device).
- * So a call never copies more than 1.1 x the bytes its frames own (c->staged[0] counts them). */
-static int stage_in(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const struct xsk_gpu_desc* dd, uint32_t n,
-                    hipStream_t st) {
+ * So a call never copies more than 1.1 x the bytes its frames own (c->staged[0] counts them).  stage_plan decides,
+ * stage_issue enqueues.  `contained`: the copy writes no mirror byte outside the chunk's own frames -- every frame
+ * 16-B aligned (a frame's read span then ends at or before the next 16-B aligned frame: include/xsk_gpu.h's
+ * ownership contract) and not the span copy; only then may it run beside another chunk's transform. */
+enum { STAGE_NONE, STAGE_2D, STAGE_SPAN, STAGE_GATHER };
+struct stage_plan {
+    int kind;
+    int contained;
+    uint64_t lo, hi, base, stride, width, sum;
+};
+static struct stage_plan stage_plan(const xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n) {
     const int wire = c->opts != 0;
-    uint64_t lo = UINT64_MAX, hi = 0, width = 0, sum = 0;
+    struct stage_plan p = {STAGE_NONE, 1, UINT64_MAX, 0, 0, 0, 0, 0};
+    uint64_t unaligned = 0;
     for (uint32_t i = 0; i < n; i++) {
+        unaligned |= d[i].addr & 15u;
         uint64_t a16 = 0;
         const uint64_t sp = xsk_gpu__read_span(d[i].addr, d[i].len, c->umem_size, wire, &a16);
         if (!sp) continue; /* the transform reads nothing of this frame */
-        if (a16 < lo) lo = a16;
-        if (a16 + sp > hi) hi = a16 + sp;
-        if (sp > width) width = sp;
-        sum += sp;
+        if (a16 < p.lo) p.lo = a16;
+        if (a16 + sp > p.hi) p.hi = a16 + sp;
+        if (sp > p.width) p.width = sp;
+        p.sum += sp;
     }
-    if (!sum) return 0;
-    const uint64_t budget = sum + sum / 10;
-    const uint64_t s = uniform_stride(d, n);
-    const uint64_t base = d[0].addr & ~15ull;
+    if (!p.sum) return p;
+    const uint64_t budget = p.sum + p.sum / 10;
+    p.stride = uniform_stride(d, n);
+    p.base = d[0].addr & ~15ull;
+    p.contained = unaligned == 0;
     /* an RX-loop-sized batch takes the gather kernel whatever its layout: one launch beats a DMA submission there
      * (64 x 64 B: 55.7 us per call vs 66.1 with the 2-D copy; 1024 x 1500 B: 126.2 vs 129.0 --
      * profiles/r04/pass1/hostlat_*.jsonl) */
     const int small = n <= XSK_GPU_LOWLAT_MAX && c->m_umem;
-    if (!small && s && width <= s && (uint64_t)n * width <= budget && base + (uint64_t)(n - 1) * s + width <= c->umem_size) {
-        if (hipMemcpy2DAsync(c->d_umem + base, s, c->umem + base, s, width, n, hipMemcpyHostToDevice, st) != hipSuccess)
-            return -EIO;
-        c->staged[0] += (uint64_t)n * width;
-        c->staged[1]++;
-        return 0;
+    const uint64_t s = p.stride;
+    if (!small && s && p.width <= s && (uint64_t)n * p.width <= budget &&
+        p.base + (uint64_t)(n - 1) * s + p.width <= c->umem_size)
+        p.kind = STAGE_2D;
+    else if (!small && (p.hi - p.lo <= budget || !c->m_umem)) { /* (no mapped alias: the span, ordered) */
+        p.kind = STAGE_SPAN;
+        p.contained = 0;
+    } else
+        p.kind = STAGE_GATHER;
+    return p;
+}
+static int stage_issue(xsk_gpu_ctx* c, const struct stage_plan* p, const struct xsk_gpu_desc* dd, uint32_t n,
+                       hipStream_t st) {
+    switch (p->kind) {
+        case STAGE_2D:
+            if (hipMemcpy2DAsync(c->d_umem + p->base, p->stride, c->umem + p->base, p->stride, p->width, n,
+                                 hipMemcpyHostToDevice, st) != hipSuccess)
+                return -EIO;
+            c->staged[0] += (uint64_t)n * p->width;
+            c->staged[1]++;
+            return 0;
+        case STAGE_SPAN:
+            if (hipMemcpyAsync(c->d_umem + p->lo, c->umem + p->lo, p->hi - p->lo, hipMemcpyHostToDevice, st) != hipSuccess)
+                return -EIO;
+            c->staged[0] += p->hi - p->lo;
+            c->staged[2]++;
+            return 0;
+        case STAGE_GATHER: {
+            const int rc = xsk_gpu__stage_gather_dev(c->m_umem, c->d_umem, c->umem_size, dd, n, (uint32_t)(c->opts != 0), st);
+            if (rc) return rc;
+            c->staged[0] += p->sum;
+            c->staged[3]++;
+            return 0;
+        }
+        default:
+            return 0;
     }
-    if (!small && (hi - lo <= budget || !c->m_umem)) { /* (no mapped alias: the span, ordered after the previous pack) */
-        if (hipMemcpyAsync(c->d_umem + lo, c->umem + lo, hi - lo, hipMemcpyHostToDevice, st) != hipSuccess) return -EIO;
-        c->staged[0] += hi - lo;
-        c->staged[2]++;
-        return 0;
-    }
-    const int rc = xsk_gpu__stage_gather_dev(c->m_umem, c->d_umem, c->umem_size, dd, n, (uint32_t)wire, st);
-    if (rc) return rc;
-    c->staged[0] += sum;
-    c->staged[3]++;
-    return 0;
 }
 
-/* Enqueue one chunk [i0, i0+n) of the batch on stream st; results land in the pinned host buffers
+/* Enqueue one chunk [i0, i0+n) of the batch (ZEROCOPY: on stream s); results land in the pinned host buffers
  * and c->done[ci] fires when they are there. */
 static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t i0, uint32_t n, uint32_t ci,
                          int want_recs, int s) {
     int rc = 0;
-    const hipStream_t st = c->stream[s];
     if (zerocopy(c)) { /* descriptors in, verdicts and counters out: mapped host memory */
+        const hipStream_t st = c->stream[s];
         memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
         memset(&c->h_stats[ci], 0, sizeof c->h_stats[ci]);
         const uint32_t tile = n <= XSK_GPU_LOWLAT_MAX ? xsk_gpu__small_tile_w(descs + i0, n, 256u) : 0u;
@@ -363,30 +424,37 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
         TRY(hipEventRecord(c->done[ci], st));
         return 0;
     }
+    /* STAGED: the copy stream (stream[0]) takes every chunk's descriptors and copy-in back to back, so the H2D
+     * direction of the link never waits for a transform; the compute stream (stream[1]) runs each chunk's
+     * transform once its copy-in is in, then its header pack and the copy-back.  A copy-in that may write mirror
+     * bytes of other chunks' frames (not contained: an unaligned frame's span reaches into its neighbour, the span
+     * copy covers whatever lies between) first waits for the previous chunk's pack, and so for every earlier
+     * chunk's (the compute stream is in order); later chunks' transforms follow their own copy-ins, which follow
+     * this one on the copy stream.  Contained copy-ins run under the other chunks' transforms. */
+    (void)s;
+    const hipStream_t sa = c->stream[0], sb = c->stream[1];
     struct xsk_gpu_desc* dd = c->d_descs + i0;
-    TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, st));
-    TRY(hipMemsetAsync(c->d_stats + ci, 0, sizeof(struct xsk_gpu_stats), st));
-    if (c->mode == XSK_GPU_MODE_STAGED) {
-        /* the previous chunk (other stream) has packed its rewritten headers before this copy-in may overwrite
-         * any mirror byte near them */
-        if (ci > 0) TRY(hipStreamWaitEvent(st, c->packed[ci - 1], 0));
-        rc = stage_in(c, descs + i0, dd, n, st);
-        if (rc) goto out;
-    }
-    rc = xsk_gpu_echo_dev_opts(c->d_umem, c->umem_size, dd, n, c->opts, c->d_verdicts + i0,
-                               want_recs ? c->d_recs + i0 : NULL, c->d_stats + ci, c->d_ws[s], st);
+    TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, sa));
+    const struct stage_plan p = stage_plan(c, descs + i0, n);
+    if (ci > 0 && !p.contained) TRY(hipStreamWaitEvent(sa, c->packed[ci - 1], 0));
+    if (p.contained) c->staged[4]++;
+    rc = stage_issue(c, &p, dd, n, sa);
     if (rc) goto out;
-    if (c->mode == XSK_GPU_MODE_STAGED) {
-        rc = xsk_gpu__pack_headers_dev(c->d_umem, dd, c->d_verdicts + i0, n, c->d_pack + (size_t)i0 * PACK,
-                                       c->opts != 0, st);
-        if (rc) goto out;
-        TRY(hipEventRecord(c->packed[ci], st));
-        TRY(hipMemcpyAsync(c->h_pack + (size_t)i0 * PACK, c->d_pack + (size_t)i0 * PACK, (size_t)n * PACK,
-                           hipMemcpyDeviceToHost, st));
-    }
-    TRY(hipMemcpyAsync(c->h_verd + i0, c->d_verdicts + i0, n, hipMemcpyDeviceToHost, st));
-    TRY(hipMemcpyAsync(c->h_stats + ci, c->d_stats + ci, sizeof *c->h_stats, hipMemcpyDeviceToHost, st));
-    TRY(hipEventRecord(c->done[ci], st));
+    TRY(hipEventRecord(c->in_done[ci], sa));
+    TRY(hipStreamWaitEvent(sb, c->in_done[ci], 0));
+    TRY(hipMemsetAsync(c->d_stats + ci, 0, sizeof(struct xsk_gpu_stats), sb));
+    rc = xsk_gpu_echo_dev_opts(c->d_umem, c->umem_size, dd, n, c->opts, c->d_verdicts + i0,
+                               want_recs ? c->d_recs + i0 : NULL, c->d_stats + ci, c->d_ws[1], sb);
+    if (rc) goto out;
+    rc = xsk_gpu__pack_headers_dev(c->d_umem, dd, c->d_verdicts + i0, n, c->d_pack + (size_t)i0 * PACK, c->opts != 0,
+                                   sb);
+    if (rc) goto out;
+    TRY(hipEventRecord(c->packed[ci], sb));
+    TRY(hipMemcpyAsync(c->h_pack + (size_t)i0 * PACK, c->d_pack + (size_t)i0 * PACK, (size_t)n * PACK,
+                       hipMemcpyDeviceToHost, sb));
+    TRY(hipMemcpyAsync(c->h_verd + i0, c->d_verdicts + i0, n, hipMemcpyDeviceToHost, sb));
+    TRY(hipMemcpyAsync(c->h_stats + ci, c->d_stats + ci, sizeof *c->h_stats, hipMemcpyDeviceToHost, sb));
+    TRY(hipEventRecord(c->done[ci], sb));
 out:
     return rc;
 }
@@ -447,15 +515,16 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
     }
     TRY(hipSetDevice(c->device));
     if (c->ll) xsk_gpu__lowlat_stop(c->ll); /* a large batch: the launch path (its streams never wait on it) */
-    const uint32_t chunk = c->mode == XSK_GPU_MODE_STAGED ? CHUNK_FRAMES : n;
-    const uint32_t nchunks = (n + chunk - 1) / chunk;
-    for (uint32_t ci = 0; ci < nchunks; ci++) {
-        const uint32_t i0 = ci * chunk, m = n - i0 < chunk ? n - i0 : chunk;
-        rc = enqueue_chunk(c, descs, i0, m, ci, recs != NULL, (int)(ci % NSTREAMS));
+    const int staged = c->mode == XSK_GPU_MODE_STAGED;
+    uint32_t nchunks = 0;
+    for (uint32_t i0 = 0; i0 < n; nchunks++) {
+        const uint32_t m = staged ? stage_chunk(n, n - i0) : n;
+        rc = enqueue_chunk(c, descs, i0, m, nchunks, recs != NULL, (int)(nchunks % NSTREAMS));
         if (rc) goto drain;
+        i0 += m;
     }
-    for (uint32_t ci = 0; ci < nchunks; ci++) {
-        const uint32_t i0 = ci * chunk, m = n - i0 < chunk ? n - i0 : chunk;
+    for (uint32_t ci = 0, i0 = 0; ci < nchunks; ci++) {
+        const uint32_t m = staged ? stage_chunk(n, n - i0) : n;
         if (hipEventSynchronize(c->done[ci]) != hipSuccess) {
             rc = -EIO;
             goto drain;
@@ -474,6 +543,7 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
             stats->tx_packets += c->h_stats[ci].tx_packets;
             stats->tx_bytes += c->h_stats[ci].tx_bytes;
         }
+        i0 += m;
     }
     if (verdicts) memcpy(verdicts, c->h_verd, n);
     if (recs) {

@@ -121,8 +121,9 @@ XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
 XSK_GPU__HIDDEN void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* ctx);
 /* xsk_gpu_host.c (exported for the GPU tests, not part of the ABI): a STAGED context's copy-in record since init --
  * out[0] bytes copied host->device, out[1..3] chunks copied as one 2-D stride / one dense span / by the gather
- * kernel.  -EINVAL for other modes. */
-int xsk_gpu__staged_stats(const xsk_gpu_ctx* ctx, uint64_t out[4]);
+ * kernel, out[4] chunks whose copy-in was contained (not ordered after the previous chunk's pack).  -EINVAL for other
+ * modes. */
+int xsk_gpu__staged_stats(const xsk_gpu_ctx* ctx, uint64_t out[5]);
 
 /* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context (doorbell layout and
  * host protocol: xsk_lowlat_proto.h). */
