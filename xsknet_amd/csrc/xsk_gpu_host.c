@@ -18,12 +18,12 @@
  *             frames cover it densely, else -- AF_XDP's recycled, scattered descriptors -- a gather kernel that
  *             moves each frame's own bytes across PCIe), transformed in HBM, and only the 38 rewritten header
  *             bytes of TX_REPLY frames are copied back and scattered into the UMEM — bytes the batch does not own
- *             are never written.  Batches of more than one chunk run as a two-stream pipeline: the copy-ins of
- *             16-B aligned frames by 2-D copy or gather write only their own frames' mirror bytes and run back
- *             to back; any other copy-in (an unaligned frame's read span may reach into a neighbour's first bytes,
- *             which another chunk may just have rewritten in the mirror) waits for the previous chunk's header
- *             pack, and the chunk after it for its pack; a chunk's copy-back overlaps the next chunk's copy-in,
- *             and the host scatters chunk i while later chunks are still in flight.
+ *             are never written.  Batches of more than one chunk run as a two-stream pipeline: a copy stream
+ *             takes every chunk's copy-in back to back and a compute stream each chunk's transform, header pack
+ *             and copy-back once its copy-in has landed; a copy-in that may write another chunk's mirror bytes (an
+ *             unaligned frame's read span reaches into its neighbour's first bytes; the dense-span copy) first waits
+ *             for the previous chunk's pack.  The last chunks halve in size, and the host scatters chunk i while
+ *             later chunks are still in flight.
  */
 #define _GNU_SOURCE
 #define __HIP_PLATFORM_AMD__ 1
