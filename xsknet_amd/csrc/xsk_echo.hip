@@ -202,23 +202,51 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
             fold = true;
         }
     }
+    // A batch of more than kMaxRounds rounds per workgroup runs as consecutive launches of about kPieceRounds rounds
+    // each, over consecutive slices of its descriptors: every launch's last round scatters its windows while no
+    // workgroup of that launch still reads, where a long share writes every round's windows into other
+    // workgroups' reads (tools/split_bench.py, profiles/r04/split/: 8 M x 1500 B at 4 KiB, one launch 300.5 us per
+    // M frames, launches of 1 M 264.3; c5's 64 M at 2 KiB 19.50 -> 18.66 ms).
+    constexpr uint32_t kRound = (uint32_t)kWaves6 * kRefTPW, kMaxRounds = 4, kPieceRounds = 2;
+    const uint32_t ntiles = (n + tl - 1) / tl;
+    uint32_t pieces = 1;
+    if (!small && (tiles_per_wg + kRound - 1) / kRound > kMaxRounds)
+        pieces = ((tiles_per_wg + kRound - 1) / kRound + kPieceRounds - 1) / kPieceRounds;
+    const uint32_t piece_tiles = (ntiles + pieces - 1) / pieces;
     const int slot = timer_begin(device, s);
-    if (opts == 0 && !small)
-        echo_round_kernel<false, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    else if (opts == 0)  // rounds of sub-tiles, writes as soon as a wave has read
-        echo_round_kernel<false, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    else if (!small)  // wire mode: the reference mode's 64-B windows and rounds, wire_header_phase64
-        echo_round_kernel<true, false><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    else
-        echo_round_kernel<true, true><<<dim3(grid), dim3(kThreads6), 0, s>>>(args, tiles_per_wg);
-    const hipError_t le = hipGetLastError();
-    timer_end(slot, s);
-    if (le != hipSuccess) return xsk_gpu__hip_fail(le);
-    if (fold) {
-        hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, s, (const unsigned long long*)d_workspace, grid,
-                           d_stats);
-        HIP_TRY(hipGetLastError());
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += piece_tiles) {
+        EchoArgs pa = args;
+        const uint64_t i0 = (uint64_t)t0 * tl;
+        pa.n = (uint32_t)(n - i0 < (uint64_t)piece_tiles * tl ? n - i0 : (uint64_t)piece_tiles * tl);
+        pa.descs = d_descs + i0;
+        pa.verdicts = d_verdicts ? d_verdicts + i0 : nullptr;
+        pa.recs = d_recs ? d_recs + i0 : nullptr;
+        uint32_t pg = grid, ptw = tiles_per_wg;
+        if (pieces > 1) echo6_geometry(pa.n, grid_force ? grid_force : ncu, &pg, &ptw);
+        if (opts == 0 && !small)
+            echo_round_kernel<false, false><<<dim3(pg), dim3(kThreads6), 0, s>>>(pa, ptw);
+        else if (opts == 0)  // rounds of sub-tiles, writes as soon as a wave has read
+            echo_round_kernel<false, true><<<dim3(pg), dim3(kThreads6), 0, s>>>(pa, ptw);
+        else if (!small)  // wire mode: the reference mode's 64-B windows and rounds, wire_header_phase64
+            echo_round_kernel<true, false><<<dim3(pg), dim3(kThreads6), 0, s>>>(pa, ptw);
+        else
+            echo_round_kernel<true, true><<<dim3(pg), dim3(kThreads6), 0, s>>>(pa, ptw);
+        const hipError_t le = hipGetLastError();
+        if (le != hipSuccess) {
+            timer_end(slot, s);
+            return xsk_gpu__hip_fail(le);
+        }
+        if (fold) {  // (the partial rows are reused by the next piece's launch, after this fold on the same stream)
+            hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(1024), 0, s, (const unsigned long long*)d_workspace,
+                               pg, d_stats);
+            const hipError_t fe = hipGetLastError();
+            if (fe != hipSuccess) {
+                timer_end(slot, s);
+                return xsk_gpu__hip_fail(fe);
+            }
+        }
     }
+    timer_end(slot, s);
     return 0;
 }
 
