@@ -565,8 +565,11 @@ def gpu_classify(umem, descs, bound):
 
 @pytest.mark.parametrize("bound", [True, False])
 @pytest.mark.parametrize("n,lo,hi,stride", [(1, 0, 200, 256), (255, 0, 200, 256), (257, 0, 200, 256),
-                                            (100000, 0, 1500, 1536), (70000, 64, 64, 64)])
+                                            (1025, 0, 200, 256), (100000, 0, 1500, 1536), (70000, 64, 64, 64),
+                                            (3_000_000, 20, 64, 64)])
 def test_classify_parity(n, lo, hi, stride, bound):
+    """Actions and the in-order REDIRECT list against the oracle, from one frame to 3 M (11 719 workgroups of the
+    classify and scatter launches)."""
     umem = np.zeros(n * stride, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, stride, seed=0x5EED0C0C + n, mode=1, len_lo=lo, len_hi=hi)
     a_ref, r_ref = oracle.xdp_classify_batch(umem, descs, bound)
