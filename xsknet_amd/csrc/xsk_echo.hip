@@ -210,7 +210,7 @@ static int echo_launch(void* d_umem, uint64_t umem_size, const struct xsk_gpu_de
     constexpr uint32_t kRound = (uint32_t)kWaves6 * kRefTPW, kMaxRounds = 4, kPieceRounds = 2;
     const uint32_t ntiles = (n + tl - 1) / tl;
     uint32_t pieces = 1;
-    if (!small && (tiles_per_wg + kRound - 1) / kRound > kMaxRounds)
+    if (!small && !args.stats_plain && (tiles_per_wg + kRound - 1) / kRound > kMaxRounds)  // (plain: one writer)
         pieces = ((tiles_per_wg + kRound - 1) / kRound + kPieceRounds - 1) / kPieceRounds;
     const uint32_t piece_tiles = (ntiles + pieces - 1) / pieces;
     const int slot = timer_begin(device, s);
