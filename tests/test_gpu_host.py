@@ -389,3 +389,20 @@ def test_lowlat_contexts_per_device_limit():
     finally:
         for c in again:
             c.close()
+
+
+@pytest.mark.parametrize("mode", [X.MODE_ZEROCOPY, X.MODE_STAGED])
+def test_long_batch_split_launches_host_counters(mode):
+    """A host batch of 2.5 M packed 64-B frames of mixed traffic in ONE call: on 256 CUs the zerocopy share is five
+    rounds, so the call runs as three launches of about two rounds, each folding its per-workgroup counter rows
+    into the mapped host slot after the previous fold (xsk_echo.hip: echo_launch); STAGED cuts it into chunks first.
+    Every byte, verdict, record and counter exact."""
+    _dev()
+    n = 2_500_000
+    umem = np.zeros(n * 64, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 64, 0x5EED5252, mode=1, len_lo=20, len_hi=64,
+                               threads=min(16, oracle.cpu_threads()))
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=n, mode=mode) as ctx:
+        v, r, st = ctx.process(descs)
+    check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
