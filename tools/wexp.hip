@@ -48,6 +48,8 @@
 //            contiguous, 4+2>, 63 <8, contiguous, 12>, 64 <16, contiguous, 12>; 65: 62 with the windows of
 //            every 2 tiles of a wave written after them (2 write phases per share, no sync); 66: 65 with a
 //            workgroup barrier before each write phase
+//   mode 68 / 69: 65 with a grid barrier before / before and after the mid-share write phase
+//   mode 67: 62 with every wave's second tile's windows written mid-share (a quarter), the rest at the end
 //   mode 70-73 (DEFER): 62's single end phase with the first half share's windows parked in a contiguous side buffer
 //            between (70 default stores, 71 nontemporal, 72 write-through, 73 = 70 without the end barrier)
 #include <hip/hip_runtime.h>
@@ -284,6 +286,19 @@ __global__ __launch_bounds__(NW * 64) void wexp_pers(const uint8_t* buf, uint32_
 // FRONT: the grid's waves sweep the batch in passes of grid * NW tiles, else contiguous per-workgroup
 // shares; LM 0: a step's 6 row-loads in one batch, 1: batches of 4 + 2 (the shipped U = 4), 2: step
 // s + 1's 6 loads issued before step s is summed (12 in flight).
+// Grid-wide barrier of a persistent grid (every workgroup resident: one per CU) on a counter that is never reset:
+// each use adds gridDim.x arrivals, so the target is the next multiple of gridDim.x.  Stores before it are waited for.
+__device__ __forceinline__ void grid_barrier(unsigned long long* ctr) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long old = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long target = (old / gridDim.x + 1ull) * gridDim.x;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+}
+
 template <int NW, bool FRONT, int LM, int ENDW = 0>
 __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n, uint32_t stride, uint32_t len,
                                                        unsigned long long* out, uint8_t* side = nullptr) {
@@ -295,7 +310,7 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
     for (uint32_t c = wave; c < per; c += NW) {
         // ENDW 4-7 (DEFER): the windows of the share's first half ("round 0", c < 2 NW) go to a contiguous side
         // buffer right after the tile (4 KiB per tile, coalesced); every window is scattered in one end phase
-        if (ENDW >= 4 && c >= 2u * NW && c < 4u * NW) {
+        if (ENDW >= 4 && ENDW <= 7 && c >= 2u * NW && c < 4u * NW) {
             const uint32_t tp = blockIdx.x * per + c - 2u * NW;  // the round-0 tile this wave read two tiles ago
             const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
             if (tp < ntiles) {
@@ -309,8 +324,18 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
             }
         }
         const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
-        if ((ENDW == 2 || ENDW == 3) && c >= 2u * NW && ((c / NW) & 1u) == 0u) {  // a write phase after every 2 tiles
+        if (ENDW == 8 && c >= 3u * NW && c < 4u * NW) {  // ENDW 8: only tile 1 of the wave written mid-share
+            const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
+            const uint32_t tt = blockIdx.x * per + c - 2u * NW;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                const uint32_t f = tt * 64u + (uint32_t)rr * 16u + (lane >> 2);
+                if (tt < ntiles && f < n) *(u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u)) = w;
+            }
+        }
+        if ((ENDW == 2 || ENDW == 3 || ENDW == 9 || ENDW == 10) && c >= 2u * NW && ((c / NW) & 1u) == 0u) {  // a write phase after every 2 tiles
             if (ENDW == 3) __syncthreads();
+            if (ENDW >= 9) grid_barrier(out + 1);  // 9 / 10: every workgroup has read its first half before any writes
             const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
             for (uint32_t cc = c - 2u * NW; cc < c; cc += NW) {
                 const uint32_t tt = blockIdx.x * per + cc;
@@ -320,6 +345,7 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
                     if (tt < ntiles && f < n) *(u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u)) = w;
                 }
             }
+            if (ENDW == 10) grid_barrier(out + 1);  // ... and no workgroup reads again before every write phase is done
         }
         if (t >= ntiles) continue;
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(buf + (uint64_t)t * 64u * stride),
@@ -368,15 +394,16 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
     if (ENDW) {  // every frame's 64-B window written once, after the workgroup has read its whole share
         if (ENDW != 2 && ENDW != 7) __syncthreads();
         const u32x4 w = u32x4{(uint32_t)acc, (uint32_t)(acc >> 32), lane, wave};
-        for (uint32_t c = (ENDW == 2 || ENDW == 3) ? wave + ((per - wave + NW - 1) / NW - 1) / 2 * 2 * NW : wave; c < per;
+        for (uint32_t c = (ENDW == 2 || ENDW == 3 || ENDW == 9 || ENDW == 10) ? wave + ((per - wave + NW - 1) / NW - 1) / 2 * 2 * NW : wave; c < per;
              c += NW) {
             const uint32_t t = FRONT ? (c / NW) * gridDim.x * NW + blockIdx.x * NW + wave : blockIdx.x * per + c;
             if (t >= ntiles) continue;
+            if (ENDW == 8 && c >= NW && c < 2u * NW) continue;  // tile 1: written mid-share
             u32x4 ws[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 ws[r] = w;
-                if (ENDW >= 4 && c < 2u * NW) ws[r] = *(const u32x4*)(side + (uint64_t)t * 4096u + (uint32_t)r * 1024u + lane * 16u);
+                if (ENDW >= 4 && ENDW <= 7 && c < 2u * NW) ws[r] = *(const u32x4*)(side + (uint64_t)t * 4096u + (uint32_t)r * 1024u + lane * 16u);
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -391,6 +418,7 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
 extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32_t len, void* out, uint32_t grid,
                         void* stream, void* side_) {
     uint8_t* side = (uint8_t*)side_;
+    if (!side && (mode == 8 || (mode >= 70 && mode <= 73))) return -1;  // modes that write or read the side buffer
     const dim3 g(grid), b(256);
     hipStream_t s = (hipStream_t)stream;
     uint8_t* p = (uint8_t*)buf;
@@ -449,6 +477,12 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 66: wexp_ladder<16, false, 1, 3><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         // 70-73 (DEFER): 62's single end phase, the first half share's windows parked in a contiguous side buffer
         // between (70 default stores, 71 nontemporal, 72 sc1 write-through, 73 = 70 without the end barrier)
+        // 68 / 69: 65 with a grid barrier before (68) / before and after (69) the mid-share write phase (the grid must be
+        // resident at once: at most one 1024-lane workgroup per CU)
+        case 68: if (grid > 256) return -1; wexp_ladder<16, false, 1, 9><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        case 69: if (grid > 256) return -1; wexp_ladder<16, false, 1, 10><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
+        // 67: 62 with a quarter of the windows (every wave's second tile) written mid-share, the rest at the end
+        case 67: wexp_ladder<16, false, 1, 8><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 70: wexp_ladder<16, false, 1, 4><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
         case 71: wexp_ladder<16, false, 1, 5><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
         case 72: wexp_ladder<16, false, 1, 6><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;

@@ -31,6 +31,9 @@
 // ONE scatter at the end of a two-round share: c3 286.4 vs 281.8 us, c4 191.8 vs 180.3, c2 46.6 vs 36.7; and the first
 // round's records and verdicts held in VGPRs until the second's write phase: c3 280.1 vs 278.8, c4 179.5 vs 179.3, c2
 // 34.9 vs 34.9, wire c3 286.1 vs 286.5; profiles/r04/defer/; removed)
+// (round 4 measured GBAR -- a non-final round's write phase held until every workgroup of the grid has read its round, a
+// grid arrival counter with a 20-us bound: c3 275.5 vs 274.8 us, c4 190.1 vs 180.6, c2 47.2 vs 35.6, wire c3 284.5 vs
+// 285.9; profiles/r04/writes/; removed)
 #include <errno.h>
 
 #include "../xsk_echo_device.h"
