@@ -16,9 +16,11 @@ import xsknet_amd as X  # noqa: E402
 # 0 as shipped (reference), 2 wire mode as shipped, 5 / 6 no SPLIT
 # (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4, 14 / 15 / 16 lean ranked streams (RS 2) with
 # 6 / 8 / 4 row-loads per batch, 17 / 18 no write-phase wait in the last round (reference / wire), 21 wire mode on 128-B
-# windows (the wire kernel of rounds 1-4), 22 / 23 wire as shipped with VLAN only / SLACK 0
-VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 14, 15, 16, 17, 18, 21, 22, 23]
-WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 18: X.OPT_ALL, 21: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL}
+# windows (the wire kernel of rounds 1-4), 22 / 23 wire as shipped with VLAN only / SLACK 0, 24 wire without paired
+# short tiles (the wire kernel before round 4's second session)
+VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 14, 15, 16, 17, 18, 21, 22, 23, 24]
+WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 18: X.OPT_ALL, 21: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL,
+             24: X.OPT_ALL}
 
 
 @pytest.mark.parametrize("variant,grid", [(v, 0) for v in VARIANTS] + [(21, 3)])
@@ -84,7 +86,7 @@ def test_product_switch_uniform_tiles(variant, flen):
             d_umem.copy_(to_dev(umem))
 
 
-@pytest.mark.parametrize("variant", [2, 21, 22, 23])
+@pytest.mark.parametrize("variant", [2, 21, 22, 23, 24])
 def test_product_wire_variants_on_wire_traffic(variant):
     """The wire-mode variants on the wire generator's traffic (tests/wire_frames.py: VLAN stacks, IHL 3-15 with
     options -- headers reaching past a 64-B window --, fragments, tot_len errors, padding, bad checksums,

@@ -77,6 +77,15 @@ __global__ __launch_bounds__(kThreads6, 1) void timed_round_kernel(EchoArgs a, u
     }
 }
 
+// The shipped wire kernel (64-B windows) with its short tiles read one at a time instead of in pairs (WPAIR 0).
+__global__ __launch_bounds__(kThreads6, 1) void wire_unpaired_kernel(EchoArgs a, uint32_t per) {
+    __shared__ Echo6Smem<kRefTPW, false> sm;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t_begin = blockIdx.x * per, t_end = min(ntiles, t_begin + per);
+    echo6_body<kRefTPW, 2, true, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack, 1, 0, kWin, 0>(a, t_begin,
+                                                                                                                t_end, sm);
+}
+
 extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* d_umem, uint64_t umem_size,
                                         const struct xsk_gpu_desc* d_descs, uint32_t n, uint8_t* d_verdicts,
                                         struct xsk_gpu_rec* d_recs, void* d_workspace, void* stream) {
@@ -122,6 +131,8 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         case 21: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0, 1, 0, kWireWin><<<gg, bb, 0, s>>>(args, per); break;
         case 22: args.opts = XSK_GPU_OPT_VLAN; echo_round_kernel<true, false><<<gg, bb, 0, s>>>(args, per); break;
         case 23: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0><<<gg, bb, 0, s>>>(args, per); break;
+        // 24: wire mode on 64-B windows without paired short tiles (WPAIR 0: the wire kernel before round 4's second session)
+        case 24: args.opts = XSK_GPU_OPT_ALL; wire_unpaired_kernel<<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

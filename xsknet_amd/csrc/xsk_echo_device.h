@@ -1010,24 +1010,26 @@ struct Echo6Smem {
     u32x4 desc[kTile];  // DLDS: the descriptors of a batch of <= 64 frames, delivered with its doorbell
 };
 
-// One frame's descriptor checks and stream geometry (reference mode), as the round body computes them.
+// One frame's descriptor checks and stream geometry on 64-B windows, as the round body computes them (WIRE: the
+// wire mode's -- it reads only [addr, addr + len) plus the window, and parses from 14 bytes on).
 struct FrameIn {
     uint64_t addr, a16;
-    uint32_t len, off, rowhi, lim;
+    uint32_t len, off, rowhi, lim, wend;
     bool ok, parse;
 };
+template <bool WIRE>
 __device__ __forceinline__ FrameIn frame_in(const EchoArgs& a, u32x4 dsc, bool in_n) {
     FrameIn F;
     F.addr = (uint64_t)dsc.x | ((uint64_t)dsc.y << 32);
     F.len = dsc.z;
-    const uint64_t need = F.len >= 20 ? (F.len > 38 ? F.len : 38) : F.len;  // xsk_receive.c:120-157
+    const uint64_t need = WIRE ? F.len : (F.len >= 20 ? (F.len > 38 ? F.len : 38) : F.len);  // xsk_receive.c:120-157
     F.ok = in_n && F.len <= kMaxLen && F.addr <= a.umem_size && need <= a.umem_size - F.addr;
-    F.parse = F.ok && F.len >= 20u;
+    F.parse = F.ok && F.len >= (WIRE ? 14u : 20u);
     F.a16 = F.addr & ~15ull;
     F.off = (uint32_t)F.addr & 15u;
     F.rowhi = F.parse ? F.off + F.len : 0u;
-    const uint32_t wend = F.ok ? (uint32_t)min(a.umem_size - F.a16, (uint64_t)kWin) : 0u;
-    F.lim = max(F.rowhi, F.parse ? wend : 0u);
+    F.wend = F.ok ? (uint32_t)min(a.umem_size - F.a16, (uint64_t)kWin) : 0u;
+    F.lim = max(F.rowhi, F.parse ? F.wend : 0u);
     return F;
 }
 
@@ -1038,7 +1040,7 @@ __device__ __forceinline__ FrameIn frame_in(const EchoArgs& a, u32x4 dsc, bool i
 // round pays two memory round trips instead of four, with twice the bytes in flight.  The windows go to the
 // two LDS slots, the ICMP sums to the two sum rows, then the header phase of each tile.  Returns false
 // (nothing written) when either tile has a longer frame.
-template <int HEAVY>
+template <int HEAVY, bool WIRE>
 __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0, uint32_t t1, uint8_t* rows0,
                                                   uint8_t* rows1, uint32_t* sums0, uint32_t* sums1, uint32_t lane,
                                                   Counters& cnt, u32x4* rec, uint32_t* verd, uint32_t* alo,
@@ -1048,7 +1050,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
     u32x4 d0 = u32x4{0u, 0u, 0u, 0u}, d1 = u32x4{0u, 0u, 0u, 0u};
     if (in0) d0 = *(const u32x4*)(a.descs + fi0);
     if (in1) d1 = *(const u32x4*)(a.descs + fi1);
-    const FrameIn F0 = frame_in(a, d0, in0), F1 = frame_in(a, d1, in1);
+    const FrameIn F0 = frame_in<WIRE>(a, d0, in0), F1 = frame_in<WIRE>(a, d1, in1);
     if ((__ballot(F0.lim > (uint32_t)kWin) | __ballot(F1.lim > (uint32_t)kWin)) != 0ull) return false;
     const uint32_t kk = lane & 3u, ro = 16u * kk;
     u32x4 x0[4], x1[4];
@@ -1096,11 +1098,15 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    bool wb = header_phase_ref(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, in0, F0.ok, F0.parse, cnt,
-                               &rec[0], &verd[0]);
+    bool wb = WIRE ? wire_header_phase64(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, F0.ok, in0, F0.wend, cnt,
+                                         &rec[0], &verd[0])
+                   : header_phase_ref(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, in0, F0.ok, F0.parse, cnt,
+                                      &rec[0], &verd[0]);
     wbm[0] = __ballot(wb);
-    wb = header_phase_ref(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, in1, F1.ok, F1.parse, cnt, &rec[1],
-                          &verd[1]);
+    wb = WIRE ? wire_header_phase64(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, F1.ok, in1, F1.wend, cnt, &rec[1],
+                                    &verd[1])
+              : header_phase_ref(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, in1, F1.ok, F1.parse, cnt, &rec[1],
+                                 &verd[1]);
     wbm[1] = __ballot(wb);
     alo[0] = d0.x;
     ahi[0] = d0.y;
@@ -1143,7 +1149,8 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0, int WW = kWireWin>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0, int WW = kWireWin,
+          int WPAIR = 1>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
                                            Echo6Smem<TPW, WIRE && WW != kWin>& sm) {
     // WW: wire mode's LDS window -- 128 B (the whole parsed header in LDS, the stream summing bytes from 128 on, one
@@ -1155,7 +1162,8 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
     static_assert(SLACK >= 0 && SLACK < kWaves6, "SLACK: waves a heavy wave does not wait for");
     constexpr int U = kU;
     constexpr bool REF = !SW;                            // reference-form stream choices (D2 / MID / SKM)
-    constexpr bool PAIR = !WIRE && TPW == 2 && !SUBT;    // paired short tiles (header_phase_ref)
+    // paired short tiles (header_phase_ref; in wire mode on 64-B windows wire_header_phase64 unless WPAIR == 0)
+    constexpr bool PAIR = !SW && TPW == 2 && !SUBT && (!WIRE || WPAIR);
     constexpr uint32_t kRowW = SW ? (uint32_t)kWireWin : (uint32_t)kWin;  // LDS row (header window) bytes
     auto& s_hdr = sm.hdr;
     uint32_t& s_arrive = sm.arrive;
@@ -1180,7 +1188,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         // ================= read phase =================
         bool paired = false;
         if (PAIR && r0 + wave < t_end && r0 + (uint32_t)kWaves6 + wave < t_end)  // wave-uniform
-            paired = read_round_short2<HEAVY>(a, r0 + wave, r0 + (uint32_t)kWaves6 + wave, s_hdr[wave][0],
+            paired = read_round_short2<HEAVY, WIRE>(a, r0 + wave, r0 + (uint32_t)kWaves6 + wave, s_hdr[wave][0],
                                               s_hdr[wave][TPW > 1 ? 1 : 0], sm.sum[wave][0], sm.sum[wave][1], lane,
                                               cnt, rec, verd, alo, ahi, wbm, round_long);
 #pragma unroll
