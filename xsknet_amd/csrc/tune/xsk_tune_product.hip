@@ -34,6 +34,9 @@
 // (round 4 measured GBAR -- a non-final round's write phase held until every workgroup of the grid has read its round, a
 // grid arrival counter with a 20-us bound: c3 275.5 vs 274.8 us, c4 190.1 vs 180.6, c2 47.2 vs 35.6, wire c3 284.5 vs
 // 285.9; profiles/r04/writes/; removed)
+// (round 4 measured PDSC -- the descriptors a failed pairing attempt loaded reused by the tiles' own streams instead of
+// reloaded, 119 VGPRs: c3 273.5 vs 273.5 us, c4 181.5 vs 180.3, c2 34.6 vs 34.5, p98 63.4 vs 64.4, wire c3 276.4 vs
+// 276.9; profiles/r04/pdsc/; removed)
 #include <errno.h>
 
 #include "../xsk_echo_device.h"
