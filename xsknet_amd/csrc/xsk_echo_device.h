@@ -848,6 +848,14 @@ __device__ __forceinline__ uint64_t sum_row_range(const uint8_t* rb, uint32_t lo
     return acc;
 }
 
+// Tag types for the two instantiations of the IPv4 gates below (untagged frame: every field at a constant offset).
+struct WireAt14 {
+    static constexpr bool kPlain = true;
+};
+struct WireAtL3 {
+    static constexpr bool kPlain = false;
+};
+
 __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* row, uint32_t ic_raw, uint64_t addr,
                                                     uint32_t len, bool ok, bool live, uint32_t wend, Counters& cnt,
                                                     u32x4* rec_out, uint32_t* verd_out) {
@@ -860,13 +868,43 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
     // frame byte i (i < len, so inside the UMEM): the window, or memory behind it
     auto fb = [&](uint32_t i) -> uint32_t { return off + i < (uint32_t)kWin ? (uint32_t)p[i] : (uint32_t)g[i]; };
     auto be16 = [&](uint32_t i) -> uint32_t { return (fb(i) << 8) | fb(i + 1); };
+    // the frame's first 40 bytes as frame-relative LE dwords (window bytes off .. off + 43 < 64): an untagged frame's
+    // fields at constant offsets come from registers instead of one LDS byte read each
+    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+    uint32_t h[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+    auto hb = [&](uint32_t i) -> uint32_t { return (h[i >> 2] >> (8u * (i & 3u))) & 0xFFu; };  // i < 40, constant
+    auto hbe16 = [&](uint32_t i) -> uint32_t { return (hb(i) << 8) | hb(i + 1u); };
     uint32_t verdict = XSK_GPU_TX_REPLY;
     uint32_t l3 = 14, hl = 20, end = len, et = 0, tags = 0;
     bool hdrs = false;
+    // the IPv4 / ICMP gates after the tags (untagged: l3 = 14, every byte from h[])
+    auto ipv4_gates = [&](auto at) {
+        constexpr bool PL = decltype(at)::kPlain;
+        auto B = [&](uint32_t k) -> uint32_t { return PL ? hb(14u + k) : fb(l3 + k); };
+        auto BE = [&](uint32_t k) -> uint32_t { return PL ? hbe16(14u + k) : be16(l3 + k); };
+        bool bad = false;
+        if (strict) {
+            const uint32_t vihl = B(0);
+            if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
+            else {
+                hl = 4u * (vihl & 15u);
+                const uint32_t tot = BE(2);
+                if (tot < hl + 8 || l3 + tot > len) bad = true;
+                else if (BE(6) & 0x3FFFu) bad = true;
+                else end = l3 + tot;
+            }
+        }
+        if (bad) verdict = XSK_GPU_DROP_BAD_IP;
+        else if (B(9) != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
+        else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
+        else hdrs = true;
+    };
     if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
     else if (len < 14) verdict = XSK_GPU_DROP_SHORT;
     else {
-        et = be16(12);
+        et = hbe16(12);
         bool cut = false;
         if (vlan) {
 #pragma unroll
@@ -884,35 +922,16 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
         if (cut) verdict = XSK_GPU_DROP_SHORT;
         else if (et != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;
         else if (len < l3 + 20) verdict = XSK_GPU_DROP_SHORT;
-        else {
-            bool bad = false;
-            if (strict) {
-                const uint32_t vihl = fb(l3);
-                if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
-                else {
-                    hl = 4u * (vihl & 15u);
-                    const uint32_t tot = be16(l3 + 2);
-                    if (tot < hl + 8 || l3 + tot > len) bad = true;
-                    else if (be16(l3 + 6) & 0x3FFFu) bad = true;
-                    else end = l3 + tot;
-                }
-            }
-            if (bad) verdict = XSK_GPU_DROP_BAD_IP;
-            else if (fb(l3 + 9) != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
-            else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
-            else hdrs = true;
-        }
+        else if (tags == 0u) ipv4_gates(WireAt14{});
+        else ipv4_gates(WireAtL3{});
     }
     const uint32_t l4 = l3 + hl;
+    const bool std34 = tags == 0u && hl == 20u;  // l3 = 14, l4 = 34: the reference's offsets
     uint32_t ip_sum = 0, ic_sum = 0, itype = 0, icode = 0, csum_in = 0, flags = 0;
     if (hdrs) {
-        if (l3 == 14u && l4 == 34u && end == len) {
-            // plain: the IPv4 header [14, 34) from the window (frame-relative dwords, as header_phase_ref) and the
+        if (std34 && end == len) {
+            // plain: the IPv4 header [14, 34) from the frame-relative dwords (as header_phase_ref) and the
             // message [34, len) from the stream
-            const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
-            uint32_t h[9];
-#pragma unroll
-            for (int k = 3; k < 9; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
             uint32_t acc = dot2_halves(h[3] >> 16, dot2_halves(h[4], dot2_halves(h[5], 0u)));
             acc = dot2_halves(h[8] & 0xFFFFu, dot2_halves(h[7], dot2_halves(h[6], acc)));
             ip_sum = bswap16(fold32(acc));
@@ -927,9 +946,9 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
                 ic_sum = bswap16(ic_sum);
             }
         }
-        itype = fb(l4);
-        icode = fb(l4 + 1);
-        csum_in = be16(l4 + 2);
+        itype = std34 ? hb(34) : fb(l4);
+        icode = std34 ? hb(35) : fb(l4 + 1);
+        csum_in = std34 ? hbe16(36) : be16(l4 + 2);
         if (ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
         if (ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
         if (tags) flags |= XSK_GPU_F_VLAN;
@@ -938,7 +957,7 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
         else if (verify && (ip_sum != 0xFFFFu || ic_sum != 0xFFFFu)) verdict = XSK_GPU_DROP_BAD_CSUM;
     }
     const bool tx = hdrs && verdict == XSK_GPU_TX_REPLY;
-    const uint32_t vihl = hdrs ? fb(l3) : 0u, proto = hdrs ? 1u : 0u;
+    const uint32_t vihl = hdrs ? (tags == 0u ? hb(14) : fb(l3)) : 0u, proto = hdrs ? 1u : 0u;
     uint32_t csum_out = csum_in;
     bool wb = false;
     if (tx) {
@@ -949,33 +968,63 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
         c16 += c16 < 0xFFF7u ? 1u : 0u;
         const uint32_t csum_new_le = (~c16) & 0xFFFFu;
         csum_out = bswap16(csum_new_le);
-        // xsk_receive.c:148-157 at the parsed offsets: MACs and addresses lie in the window (off + l3 + 20 <= 57)
+        if (std34) {
+            // the reference's offsets: the rewrite of xsk_receive.c:148-157 as header_phase_ref's dword shuffles
+            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
+            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
+            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
+            const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
+            const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
+            const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
+            if (off == 0u && wend >= (uint32_t)kWin) {
+                uint32_t* r32 = (uint32_t*)row;  // patched in LDS, stored as a whole window in the write phase
+                r32[0] = n0;
+                r32[1] = n1;
+                r32[2] = n2;
+                r32[6] = n6;
+                r32[7] = n7;
+                r32[8] = n8;
+                r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+                wb = true;
+            } else {  // byte-exact: only the rewritten bytes
+                uint8_t* pkt = a.umem + addr;
+                const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            const uint8_t x = p[i];
-            p[i] = p[6 + i];
-            p[6 + i] = x;
-        }
+                for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint8_t x = p[l3 + 12 + i];
-            p[l3 + 12 + i] = p[l3 + 16 + i];
-            p[l3 + 16 + i] = x;
-        }
-        if (off == 0u && l4 + 4u <= (uint32_t)kWin && wend >= (uint32_t)kWin) {
-            p[l4] = 0;  // whole 64-B sector, stored in the write phase
-            p[l4 + 2] = (uint8_t)csum_new_le;
-            p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
-            wb = true;
-        } else {  // byte-exact: only the rewritten bytes
-            uint8_t* pkt = a.umem + addr;
+                for (int b = 26; b < 35; ++b) pkt[b] = (uint8_t)(w[3 + ((b - 24) >> 2)] >> (8 * (b & 3)));
+                pkt[36] = (uint8_t)csum_new_le;
+                pkt[37] = (uint8_t)(csum_new_le >> 8);
+            }
+        } else {
+            // xsk_receive.c:148-157 at the parsed offsets: MACs and addresses lie in the window (off + l3 + 20 <= 57)
 #pragma unroll
-            for (int i = 0; i < 12; ++i) pkt[i] = p[i];
+            for (int i = 0; i < 6; ++i) {
+                const uint8_t x = p[i];
+                p[i] = p[6 + i];
+                p[6 + i] = x;
+            }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
-            pkt[l4] = 0;
-            pkt[l4 + 2] = (uint8_t)csum_new_le;
-            pkt[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+            for (int i = 0; i < 4; ++i) {
+                const uint8_t x = p[l3 + 12 + i];
+                p[l3 + 12 + i] = p[l3 + 16 + i];
+                p[l3 + 16 + i] = x;
+            }
+            if (off == 0u && l4 + 4u <= (uint32_t)kWin && wend >= (uint32_t)kWin) {
+                p[l4] = 0;  // whole 64-B sector, stored in the write phase
+                p[l4 + 2] = (uint8_t)csum_new_le;
+                p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+                wb = true;
+            } else {  // byte-exact: only the rewritten bytes
+                uint8_t* pkt = a.umem + addr;
+#pragma unroll
+                for (int i = 0; i < 12; ++i) pkt[i] = p[i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
+                pkt[l4] = 0;
+                pkt[l4 + 2] = (uint8_t)csum_new_le;
+                pkt[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+            }
         }
     }
     u32x4 r;
