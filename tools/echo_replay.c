@@ -4,7 +4,7 @@
  * per-descriptor process_packet() call replaced by one xsk_gpu_process() per batch.
  *
  *   echo_replay <umem.bin> <descs.bin> <out_umem.bin> <out_verdicts.bin> [batch] [zerocopy|staged|lowlat]
- *               [gpus=D0,D1,...] [reps=R] [flush=1] [huge=1]
+ *               [gpus=D0,D1,...] [reps=R] [flush=1] [huge=1] [opts=O]
  *
  * With gpus=..., the batches go through xsk_gpu_multi_process() over one context per listed device
  * (repeats allowed): descriptor i of a batch on context i mod G, counters summed on the host.
@@ -12,7 +12,8 @@
  * between passes (untimed), and one more key=value pair, us_per_call (wall clock per batch call, the
  * first pass -- which starts the device side -- excluded), is printed; the outputs are those of pass 1.
  * flush=1 evicts the restored UMEM from the CPU caches before each timed pass (frames a NIC delivered);
- * huge=1 puts the UMEM on transparent huge pages.
+ * huge=1 puts the UMEM on transparent huge pages.  opts=O sets the wire-format options (XSK_GPU_OPT_*, include/xsk_gpu.h)
+ * with xsk_gpu_set_options() / xsk_gpu_multi_set_options() before the first batch.
  *
  * umem.bin: raw UMEM bytes (size multiple of 16).  descs.bin: packed struct xdp_desc records
  * (u64 addr, u32 len, u32 options).  Prints the stats_record counters the reference's stats
@@ -91,7 +92,7 @@ int main(int argc, char** argv) {
     if (argc > 6 && strcmp(argv[6], "staged") == 0) mode = XSK_GPU_MODE_STAGED;
     if (argc > 6 && strcmp(argv[6], "lowlat") == 0) mode = XSK_GPU_MODE_LOWLAT;
     int devices[XSK_GPU_MULTI_MAX];
-    uint32_t ndev = 0, reps = 0, flush = 0, huge = 0, tile = 0, groups = 0;
+    uint32_t ndev = 0, reps = 0, flush = 0, huge = 0, tile = 0, groups = 0, opts = 0;
     for (int a = 7; a < argc; a++) {
         if (strncmp(argv[a], "gpus=", 5) == 0) {
             for (char* p = argv[a] + 5; *p && ndev < XSK_GPU_MULTI_MAX;) {
@@ -109,6 +110,8 @@ int main(int argc, char** argv) {
             tile = (uint32_t)strtoul(argv[a] + 5, NULL, 10);
         } else if (strncmp(argv[a], "groups=", 7) == 0) { /* LOWLAT: serving workgroups (--groups) */
             groups = (uint32_t)strtoul(argv[a] + 7, NULL, 10);
+        } else if (strncmp(argv[a], "opts=", 5) == 0) { /* wire-format options (--opts) */
+            opts = (uint32_t)strtoul(argv[a] + 5, NULL, 10);
         }
     }
     size_t umem_size = 0, desc_bytes = 0;
@@ -145,6 +148,10 @@ int main(int argc, char** argv) {
                   : xsk_gpu_init(&ctx, 0, umem, umem_size, batch, mode);
     if (rc) {
         fprintf(stderr, "init: %s (%s)\n", strerror(-rc), xsk_gpu_last_error());
+        return 1;
+    }
+    if (opts && (rc = multi ? xsk_gpu_multi_set_options(multi, opts) : xsk_gpu_set_options(ctx, opts))) {
+        fprintf(stderr, "options: %s\n", strerror(-rc));
         return 1;
     }
     if ((tile || groups) && ctx && mode == XSK_GPU_MODE_LOWLAT && (rc = xsk_gpu__lowlat_tune(ctx, tile, groups, 0))) {

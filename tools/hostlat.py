@@ -6,7 +6,7 @@ in batches of 64 (RX_BATCH_SIZE, xsk_utils.h:8) up to 4096 frames, for the zeroc
 (resident polling kernel) modes, and the multi-context path (``--gpus 0,0``).  Each timed pass restores the
 UMEM (untimed) so every call transforms echo requests.  Prints one JSON line per (frame length, mode, batch).
 
-  python tools/hostlat.py [--lens 64,1500] [--modes zerocopy,staged,lowlat] [--batches 64,256,1024,4096]
+  python tools/hostlat.py [--lens 64,1500] [--modes zerocopy,staged,lowlat] [--batches 64,256,1024,4096] [--opts 7]
                           [--gpus 0,0] [--reps 200] [--scramble]
 
 --scramble puts the descriptors in a random order over the UMEM's chunks: the RX ring of a client after its free stack
@@ -36,6 +36,8 @@ def run_one(exe, p, flen, mode, batch, tile, args):
         cmd.append(f"tile={tile}")
     if args.groups:
         cmd.append(f"groups={args.groups}")
+    if args.opts:
+        cmd.append(f"opts={args.opts}")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     if r.returncode != 0:
         print(json.dumps({"frame_len": flen, "mode": mode, "batch": batch, "error": r.stderr[-300:]}))
@@ -43,7 +45,7 @@ def run_one(exe, p, flen, mode, batch, tile, args):
     kv = dict(x.split("=") for x in r.stdout.split())
     us = float(kv["us_per_call"])
     rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto", "groups": args.groups or "auto",
-           "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge), "scrambled": bool(args.scramble),
+           "opts": args.opts, "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge), "scrambled": bool(args.scramble),
            "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3), "calls": int(kv["calls"])}
     if "trace_ns" in kv:  # LOWLAT: the last batch's phases on the GPU
         t = [int(x) for x in kv["trace_ns"].split(",")]
@@ -69,6 +71,7 @@ def main():
     ap.add_argument("--huge", action="store_true", help="the UMEM on transparent huge pages (2 MiB)")
     ap.add_argument("--tiles", default="", help="LOWLAT frames per wave to sweep (echo_replay tile=), e.g. 4,16,64")
     ap.add_argument("--groups", type=int, default=0, help="LOWLAT serving workgroups (echo_replay groups=; 0: by size)")
+    ap.add_argument("--opts", type=int, default=0, help="wire-format options (echo_replay opts=; 7 = every option)")
     ap.add_argument("--scramble", action="store_true", help="descriptors in a random order over the UMEM's chunks")
     args = ap.parse_args()
     exe = os.path.join(ROOT, "tools", "echo_replay")
