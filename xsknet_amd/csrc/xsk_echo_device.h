@@ -684,6 +684,14 @@ __device__ __forceinline__ bool header_phase_ref(const EchoArgs& a, uint8_t* row
 // STRICT cuts a message short of the frame beyond the window), decides, patches the reply in LDS.
 // Returns true when the patched 64-B window should leave as a whole sector (aligned, rewrite < 64 B).
 // ================================================================================================
+// Tag types for the two instantiations of the IPv4 gates of the wire header phases (untagged frame: every field at a constant offset).
+struct WireAt14 {
+    static constexpr bool kPlain = true;
+};
+struct WireAtL3 {
+    static constexpr bool kPlain = false;
+};
+
 __device__ __forceinline__ uint32_t wbe16(const uint8_t* p, uint32_t i) {
     return ((uint32_t)p[i] << 8) | (uint32_t)p[i + 1];
 }
@@ -696,13 +704,42 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
     const bool verify = (a.opts & XSK_GPU_OPT_VERIFY_CSUM) != 0u;
     const uint32_t off = (uint32_t)addr & 15u;
     uint8_t* p = row + off;  // frame byte i = p[i] for off + i < wend
+    // the frame's first 40 bytes as frame-relative LE dwords: an untagged frame's fields at constant offsets come from
+    // registers instead of one LDS byte read each (as wire_header_phase64)
+    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
+    uint32_t h[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+    auto hb = [&](uint32_t i) -> uint32_t { return (h[i >> 2] >> (8u * (i & 3u))) & 0xFFu; };  // i < 40, constant
+    auto hbe16 = [&](uint32_t i) -> uint32_t { return (hb(i) << 8) | hb(i + 1u); };
     uint32_t verdict = XSK_GPU_TX_REPLY;
     uint32_t l3 = 14, hl = 20, end = len, et = 0, tags = 0;
     bool hdrs = false;  // all three headers inside the frame: the record is filled
+    auto ipv4_gates = [&](auto at) {  // after the tags (untagged: l3 = 14, every byte from h[])
+        constexpr bool PL = decltype(at)::kPlain;
+        auto B = [&](uint32_t k) -> uint32_t { return PL ? hb(14u + k) : (uint32_t)p[l3 + k]; };
+        auto BE = [&](uint32_t k) -> uint32_t { return PL ? hbe16(14u + k) : wbe16(p, l3 + k); };
+        bool bad = false;
+        if (strict) {
+            const uint32_t vihl = B(0);
+            if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
+            else {
+                hl = 4u * (vihl & 15u);
+                const uint32_t tot = BE(2);
+                if (tot < hl + 8 || l3 + tot > len) bad = true;
+                else if (BE(6) & 0x3FFFu) bad = true;
+                else end = l3 + tot;
+            }
+        }
+        if (bad) verdict = XSK_GPU_DROP_BAD_IP;
+        else if (B(9) != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
+        else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
+        else hdrs = true;
+    };
     if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
     else if (len < 14) verdict = XSK_GPU_DROP_SHORT;
     else {
-        et = wbe16(p, 12);
+        et = hbe16(12);
         bool cut = false;
         if (vlan) {
 #pragma unroll
@@ -720,37 +757,25 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
         if (cut) verdict = XSK_GPU_DROP_SHORT;
         else if (et != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;
         else if (len < l3 + 20) verdict = XSK_GPU_DROP_SHORT;
-        else {
-            bool bad = false;
-            if (strict) {
-                const uint32_t vihl = p[l3];
-                if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
-                else {
-                    hl = 4u * (vihl & 15u);
-                    const uint32_t tot = wbe16(p, l3 + 2);
-                    if (tot < hl + 8 || l3 + tot > len) bad = true;
-                    else if (wbe16(p, l3 + 6) & 0x3FFFu) bad = true;
-                    else end = l3 + tot;
-                }
-            }
-            if (bad) verdict = XSK_GPU_DROP_BAD_IP;
-            else if (p[l3 + 9] != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
-            else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
-            else hdrs = true;
-        }
+        else if (tags == 0u) ipv4_gates(WireAt14{});
+        else ipv4_gates(WireAtL3{});
     }
     const uint32_t l4 = l3 + hl;
+    const bool std34 = tags == 0u && hl == 20u;  // l3 = 14, l4 = 34: the reference's offsets
     uint32_t ip_sum = 0, ic_sum = 0, itype = 0, icode = 0, csum_in = 0, flags = 0;
     if (hdrs) {
-        // in-window sums (absolute-alignment domain: LE dwords of the 16-B aligned row)
+        // in-window sums (absolute-alignment domain: LE dwords of the 16-B aligned row), 16 B per LDS read
         const uint32_t ic_end = off + end, ic_hi_w = min(ic_end, (uint32_t)kWireWin);
         uint64_t ip_acc = 0, ic_acc = 0;
-        const uint32_t* r32 = (const uint32_t*)row;
-#pragma unroll 8
-        for (int d = 0; d < 32; ++d) {
-            const uint32_t x = r32[d];
-            ip_acc += keep_bytes(x, 4 * d, (int)(off + l3), (int)(off + l4));
-            ic_acc += keep_bytes(x, 4 * d, (int)(off + l4), (int)ic_hi_w);
+#pragma unroll
+        for (int b = 0; b < (int)kWireWin / 16; ++b) {
+            const u32x4 x = ((const u32x4*)row)[b];
+            if (!std34) ip_acc += sum_range(x, 16 * b, (int)(off + l3), (int)(off + l4));
+            ic_acc += sum_range(x, 16 * b, (int)(off + l4), (int)ic_hi_w);
+        }
+        if (std34) {  // the IPv4 header [14, 34) from the frame-relative dwords (as header_phase_ref)
+            ip_acc = dot2_halves(h[3] >> 16, dot2_halves(h[4], dot2_halves(h[5], 0u)));
+            ip_acc = dot2_halves(h[8] & 0xFFFFu, dot2_halves(h[7], dot2_halves(h[6], (uint32_t)ip_acc)));
         }
         uint64_t far = 0;
         if (ic_end > (uint32_t)kWireWin) {
@@ -762,15 +787,21 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
                     far += keep_bytes(*(const uint32_t*)(fb + o), (int)o, kWireWin, (int)ic_end);
             }
         }
-        ip_sum = fold64(ip_acc);
-        ic_sum = fold64(ic_acc + far);
-        if (!((uint32_t)addr & 1u)) {
-            ip_sum = bswap16(ip_sum);
-            ic_sum = bswap16(ic_sum);
+        if (std34) {  // frame-relative halves: byte-swapped network words (RFC 1071 §2(B)), as header_phase_ref
+            ip_sum = bswap16(fold32((uint32_t)ip_acc));
+            ic_sum = fold64(ic_acc + far);
+            if (!((uint32_t)addr & 1u)) ic_sum = bswap16(ic_sum);
+        } else {
+            ip_sum = fold64(ip_acc);
+            ic_sum = fold64(ic_acc + far);
+            if (!((uint32_t)addr & 1u)) {
+                ip_sum = bswap16(ip_sum);
+                ic_sum = bswap16(ic_sum);
+            }
         }
-        itype = p[l4];
-        icode = p[l4 + 1];
-        csum_in = wbe16(p, l4 + 2);
+        itype = std34 ? hb(34) : p[l4];
+        icode = std34 ? hb(35) : p[l4 + 1];
+        csum_in = std34 ? hbe16(36) : wbe16(p, l4 + 2);
         if (ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
         if (ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
         if (tags) flags |= XSK_GPU_F_VLAN;
@@ -789,35 +820,65 @@ __device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* ro
         c16 += c16 < 0xFFF7u ? 1u : 0u;
         const uint32_t csum_new_le = (~c16) & 0xFFFFu;
         csum_out = bswap16(csum_new_le);
+        if (std34) {
+            // the reference's offsets: the rewrite of xsk_receive.c:148-157 as header_phase_ref's dword shuffles
+            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
+            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
+            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
+            const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
+            const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
+            const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
+            if (off == 0u && wend >= 64u) {
+                uint32_t* r32 = (uint32_t*)row;  // patched in LDS, stored as a whole 64-B sector in the write phase
+                r32[0] = n0;
+                r32[1] = n1;
+                r32[2] = n2;
+                r32[6] = n6;
+                r32[7] = n7;
+                r32[8] = n8;
+                r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+                wb = true;
+            } else {  // byte-exact: only the rewritten bytes
+                uint8_t* pkt = a.umem + addr;
+                const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {  // xsk_receive.c:148-157 at the parsed offsets, in LDS
-            const uint8_t x = p[i];
-            p[i] = p[6 + i];
-            p[6 + i] = x;
-        }
+                for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint8_t x = p[l3 + 12 + i];
-            p[l3 + 12 + i] = p[l3 + 16 + i];
-            p[l3 + 16 + i] = x;
-        }
-        p[l4] = 0;
-        p[l4 + 2] = (uint8_t)csum_new_le;
-        p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
-        if (off == 0u && l4 + 4u <= 64u && wend >= 64u) {
-            wb = true;  // whole 64-B sector, stored in the write phase
-        } else {        // byte-exact: only the rewritten bytes
-            uint8_t* pkt = a.umem + addr;
+                for (int b = 26; b < 35; ++b) pkt[b] = (uint8_t)(w[3 + ((b - 24) >> 2)] >> (8 * (b & 3)));
+                pkt[36] = (uint8_t)csum_new_le;
+                pkt[37] = (uint8_t)(csum_new_le >> 8);
+            }
+        } else {
 #pragma unroll
-            for (int i = 0; i < 12; ++i) pkt[i] = p[i];
+            for (int i = 0; i < 6; ++i) {  // xsk_receive.c:148-157 at the parsed offsets, in LDS
+                const uint8_t x = p[i];
+                p[i] = p[6 + i];
+                p[6 + i] = x;
+            }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
-            pkt[l4] = 0;
-            pkt[l4 + 2] = p[l4 + 2];
-            pkt[l4 + 3] = p[l4 + 3];
+            for (int i = 0; i < 4; ++i) {
+                const uint8_t x = p[l3 + 12 + i];
+                p[l3 + 12 + i] = p[l3 + 16 + i];
+                p[l3 + 16 + i] = x;
+            }
+            p[l4] = 0;
+            p[l4 + 2] = (uint8_t)csum_new_le;
+            p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
+            if (off == 0u && l4 + 4u <= 64u && wend >= 64u) {
+                wb = true;  // whole 64-B sector, stored in the write phase
+            } else {        // byte-exact: only the rewritten bytes
+                uint8_t* pkt = a.umem + addr;
+#pragma unroll
+                for (int i = 0; i < 12; ++i) pkt[i] = p[i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
+                pkt[l4] = 0;
+                pkt[l4 + 2] = p[l4 + 2];
+                pkt[l4 + 3] = p[l4 + 3];
+            }
         }
     }
-    const uint32_t vihl = hdrs ? p[l3] : 0u, proto = hdrs ? 1u : 0u;
+    const uint32_t vihl = hdrs ? (tags == 0u ? hb(14) : (uint32_t)p[l3]) : 0u, proto = hdrs ? 1u : 0u;
     u32x4 r;
     r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
     r.y = icode | (vihl << 8) | ((hdrs ? et : 0u) << 16);
@@ -847,14 +908,6 @@ __device__ __forceinline__ uint64_t sum_row_range(const uint8_t* rb, uint32_t lo
     for (uint32_t o = lo & ~3u; o < hi; o += 4u) acc += keep_bytes(*(const uint32_t*)(rb + o), (int)o, (int)lo, (int)hi);
     return acc;
 }
-
-// Tag types for the two instantiations of the IPv4 gates below (untagged frame: every field at a constant offset).
-struct WireAt14 {
-    static constexpr bool kPlain = true;
-};
-struct WireAtL3 {
-    static constexpr bool kPlain = false;
-};
 
 __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* row, uint32_t ic_raw, uint64_t addr,
                                                     uint32_t len, bool ok, bool live, uint32_t wend, Counters& cnt,
@@ -1514,7 +1567,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // (44 / 280 / 185 us for c2 / c3 / c4 against 71 / 298 / 215 on the 128-B windows of rounds 1-4, in-process A/B,
 // profiles/r04/wire64/).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = SUBT ? 0 : kRefSlack, int RS = 1, int LASTW = 0, int WW = (WIRE && !SUBT) ? kWin : kWireWin>
+          int SLACK = SUBT ? 0 : kRefSlack, int RS = 1, int LASTW = 0, int WW = WIRE ? kWin : kWireWin>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr bool SW = WIRE && WW != kWin;  // wire mode on 128-B windows
     constexpr int TPW = (SW || SUBT) ? 1 : kRefTPW;
