@@ -136,6 +136,8 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         case 23: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0><<<gg, bb, 0, s>>>(args, per); break;
         // 24: wire mode on 64-B windows without paired short tiles (WPAIR 0: the wire kernel before round 4's second session)
         case 24: args.opts = XSK_GPU_OPT_ALL; wire_unpaired_kernel<<<gg, bb, 0, s>>>(args, per); break;
+        // (25, one tile per wave per round -- four rounds per 1 M-frame share, a quarter of the windows in the last write
+        // phase: c2 35.9 vs 35.3 us, p98 63.5 vs 63.8, c3 287.5 vs 276.4; profiles/r04/tpw1/, removed)
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
