@@ -50,6 +50,8 @@
 //            workgroup barrier before each write phase
 //   mode 68 / 69: 65 with a grid barrier before / before and after the mid-share write phase
 //   mode 67: 62 with every wave's second tile's windows written mid-share (a quarter), the rest at the end
+//   mode 74 (REREAD): 62's single end phase, the first half share's windows read again (64 B per frame) right before
+//            they are stored in it -- the kernel form would keep only sums and verdicts of round 0 and redo its rewrite
 //   mode 70-73 (DEFER): 62's single end phase with the first half share's windows parked in a contiguous side buffer
 //            between (70 default stores, 71 nontemporal, 72 write-through, 73 = 70 without the end barrier)
 #include <hip/hip_runtime.h>
@@ -404,6 +406,11 @@ __global__ __launch_bounds__(NW * 64) void wexp_ladder(uint8_t* buf, uint32_t n,
             for (int r = 0; r < 4; ++r) {
                 ws[r] = w;
                 if (ENDW >= 4 && ENDW <= 7 && c < 2u * NW) ws[r] = *(const u32x4*)(side + (uint64_t)t * 4096u + (uint32_t)r * 1024u + lane * 16u);
+                if (ENDW == 11 && c < 2u * NW) {  // REREAD: the first half share's windows read again before they go out
+                    const uint32_t f = t * 64u + (uint32_t)r * 16u + (lane >> 2);
+                    if (f < n) ws[r] = *(const u32x4*)(buf + (uint64_t)f * stride + 16u * (lane & 3u));
+                    ws[r].x ^= w.x;
+                }
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -487,6 +494,7 @@ extern "C" int wexp_run(int mode, void* buf, uint32_t n, uint32_t stride, uint32
         case 71: wexp_ladder<16, false, 1, 5><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
         case 72: wexp_ladder<16, false, 1, 6><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
         case 73: wexp_ladder<16, false, 1, 7><<<g, 1024, 0, s>>>(p, n, stride, len, o, side); break;
+        case 74: wexp_ladder<16, false, 1, 11><<<g, 1024, 0, s>>>(p, n, stride, len, o); break;
         case 13: wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;
         case 14: wexp_kernel<14><<<g, b, 0, s>>>(p, n, stride, len, o, side);
                  wexp_patch<<<(n * 4 + 255) / 256, 256, 0, s>>>(p, n, stride); break;

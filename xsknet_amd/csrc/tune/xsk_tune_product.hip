@@ -138,6 +138,9 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         case 24: args.opts = XSK_GPU_OPT_ALL; wire_unpaired_kernel<<<gg, bb, 0, s>>>(args, per); break;
         // (25, one tile per wave per round -- four rounds per 1 M-frame share, a quarter of the windows in the last write
         // phase: c2 35.9 vs 35.3 us, p98 63.5 vs 63.8, c3 287.5 vs 276.4; profiles/r04/tpw1/, removed)
+        // (26, REREAD -- the share's second-to-last round stores records and verdicts but not its windows, which are read
+        // again, re-patched and stored after the last round's write phase: c3 284.1 vs 274.9 us, c4 190.3 vs 176.0, c2
+        // 39.6 vs 35.0, p98 74.8 vs 63.9, outputs equal; profiles/r04/reread/, removed)
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
