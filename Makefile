@@ -16,7 +16,7 @@ all: $(LIB) $(TUNELIB) oracle tools/echo_replay tools/rxqueues
 
 # every header a device object or a host object may include (the doorbell layout and host protocol of
 # xsk_lowlat_proto.h are shared by xsk_lowlat.hip and xsk_gpu_host.c)
-HDRS     := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h $(CSRC)/xsk_gpu_internal.h \
+HDRS     := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h $(CSRC)/xsk_gpu_internal.h $(CSRC)/xsk_stage_plan.h \
             $(CSRC)/xsk_lowlat_proto.h $(CSRC)/xsk_ring.h include/xsk_gpu.h
 # build id of the transform kernel: a hash of the sources that define it and of the flags, reported by
 # xsk_gpu_build_id() so bench.py attaches a PMC traffic summary only to the build it was measured on

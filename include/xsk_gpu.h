@@ -115,7 +115,7 @@ enum xsk_gpu_verdict {
 /* the frame (TX_REPLY, DROP_NOT_ECHO, DROP_BAD_CSUM), else zero: eth_proto = inner ethertype,   */
 /* ip_vihl / ip_proto / icmp_* from l3 / l4, ip_sum over [l3, l4), icmp_sum over the message,    */
 /* flags IP_CSUM_OK / ICMP_CSUM_OK (sum == 0xFFFF), VLAN, IP_OPTIONS.  Wire mode reads only      */
-/* [addr, addr + len) plus the 16-B-aligned 128-byte header window (within the UMEM), and a      */
+/* [addr, addr + len) plus the 16-B-aligned 64-byte header window (within the UMEM), and a       */
 /* descriptor whose [addr, addr + len) leaves the UMEM is DROP_BAD_DESC.                         */
 /* ------------------------------------------------------------------------------------------ */
 #define XSK_GPU_OPT_STRICT_IPV4 0x1u

@@ -124,6 +124,8 @@ _SIGS = {
     "xsk_gpu_multi_fini": ([_P], None),
     "xsk_gpu_lowlat_reserve": ([C.c_int, C.c_uint32], C.c_int),
     "xsk_gpu__staged_stats": ([_P, C.POINTER(C.c_uint64)], C.c_int),
+    "xsk_gpu__staged_noalias": ([_P, C.c_uint32], C.c_int),
+    "xsk_gpu__multi_ctx": ([_P, C.c_uint32], _P),
     # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
     "xsk_gpu__echo_dev_grid": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32], C.c_int),
 }
@@ -263,6 +265,20 @@ def timing_read():
     return ms.value, cnt.value
 
 
+STAGED_FIELDS = ("h2d_bytes", "strided", "span", "gather", "contained", "hostpack", "own_dma")
+
+
+def staged_stats_of(ctx) -> dict:
+    """xsk_gpu__staged_stats of a STAGED context handle: bytes copied host->device since init (frame bytes, plus the
+    host pack's 4-B staging offsets), the chunks copied as one 2-D stride / one dense span / by the gather kernel, the
+    chunks whose copy-in wrote only their own frames' mirror bytes (run without waiting for the previous chunk's header
+    pack), the chunks copied by the host pack (no mapped alias), and the frames of those too large for a staging half
+    (a DMA copy each)."""
+    out = (C.c_uint64 * len(STAGED_FIELDS))()
+    _check("xsk_gpu__staged_stats", lib().xsk_gpu__staged_stats(ctx, out))
+    return dict(zip(STAGED_FIELDS, (int(x) for x in out)))
+
+
 class EchoContext:
     """Host-UMEM drop-in (xsk_gpu_init / xsk_gpu_process / xsk_gpu_fini) over a numpy uint8 UMEM."""
 
@@ -297,12 +313,14 @@ class EchoContext:
         return verdicts, recs, stats[0]
 
     def staged_stats(self):
-        """xsk_gpu__staged_stats of a STAGED context: bytes copied host->device since init, and the chunks copied as
-        one 2-D stride / one dense span / by the gather kernel, and the chunks whose copy-in wrote only their own frames'
-        mirror bytes (run without waiting for the previous chunk's header pack)."""
-        out = (C.c_uint64 * 5)()
-        _check("xsk_gpu__staged_stats", lib().xsk_gpu__staged_stats(self._ctx, out))
-        return {"h2d_bytes": out[0], "strided": out[1], "span": out[2], "gather": out[3], "contained": out[4]}
+        """xsk_gpu__staged_stats of a STAGED context (see staged_stats_of)."""
+        return staged_stats_of(self._ctx)
+
+    def drop_alias(self, half_bytes: int = 0) -> None:
+        """Test switch (xsk_gpu__staged_noalias): the STAGED context forgets its UMEM's mapped device alias, as on a
+        device where the runtime gives none, so its scattered copy-ins take the host pack (staging halves of
+        half_bytes; 0 = the default 32 MiB)."""
+        _check("xsk_gpu__staged_noalias", lib().xsk_gpu__staged_noalias(self._ctx, half_bytes))
 
     def lowlat_tune(self, tile_frames: int = 0, groups: int = 0, timeout_us: int = 0) -> None:
         """Tool / test knobs of a LOWLAT context (xsk_gpu__lowlat_tune): frames per wave, serving workgroups,
@@ -368,6 +386,22 @@ class MultiContext:
         if g < 0:
             raise XskGpuError("xsk_gpu_multi_status", g)
         return list(st[:g])
+
+    def context(self, g: int):
+        """Context g's handle (xsk_gpu__multi_ctx), for staged_stats_of."""
+        h = lib().xsk_gpu__multi_ctx(self._ctx, g)
+        if not h:
+            raise XskGpuError("xsk_gpu__multi_ctx", -22)
+        return h
+
+    def staged_stats(self):
+        """Every context's xsk_gpu__staged_stats (STAGED mode), in context order."""
+        return [staged_stats_of(self.context(g)) for g in range(len(self.status()))]
+
+    def drop_alias(self, half_bytes: int = 0) -> None:
+        """Test switch: every context forgets the UMEM's mapped alias (xsk_gpu__staged_noalias)."""
+        for g in range(len(self.status())):
+            _check("xsk_gpu__staged_noalias", lib().xsk_gpu__staged_noalias(self.context(g), half_bytes))
 
     def inject_failure(self, g: int, rc: int) -> None:
         """Test hook: context g's next share fails with rc (xsk_gpu__multi_inject)."""

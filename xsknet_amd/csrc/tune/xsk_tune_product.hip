@@ -53,7 +53,7 @@ extern "C" uint32_t xsk_gpu__num_cu(int device);
 // k of workgroup g is tiles [(k * grid + g) * 32, + 32) (counters are not meaningful: one partial row per round).
 template <int PERM>
 __global__ __launch_bounds__(kThreads6, 1) void timed_round_kernel(EchoArgs a, uint32_t per, unsigned long long* wgt) {
-    __shared__ Echo6Smem<kRefTPW, false> sm;
+    __shared__ Echo6Smem<kRefTPW> sm;
     const uint64_t t0 = wall_clock64();
     const uint32_t ntiles = (a.n + kTile - 1) / kTile;
     constexpr uint32_t kRound = (uint32_t)kWaves6 * kRefTPW;
@@ -78,15 +78,6 @@ __global__ __launch_bounds__(kThreads6, 1) void timed_round_kernel(EchoArgs a, u
         wgt[4 * blockIdx.x + 2] = xcc;
         wgt[4 * blockIdx.x + 3] = hwid;
     }
-}
-
-// The shipped wire kernel (64-B windows) with its short tiles read one at a time instead of in pairs (WPAIR 0).
-__global__ __launch_bounds__(kThreads6, 1) void wire_unpaired_kernel(EchoArgs a, uint32_t per) {
-    __shared__ Echo6Smem<kRefTPW, false> sm;
-    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
-    const uint32_t t_begin = blockIdx.x * per, t_end = min(ntiles, t_begin + per);
-    echo6_body<kRefTPW, 2, true, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack, 1, 0, kWin, 0>(a, t_begin,
-                                                                                                                t_end, sm);
 }
 
 extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* d_umem, uint64_t umem_size,
@@ -121,21 +112,14 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         // 9: SLACK 0 -- heavy waves wait for every wave of the workgroup (round 3's write-phase wait); 13: SLACK 4
         case 9: echo_round_kernel<false, false, kUR, true, true, 0><<<gg, bb, 0, s>>>(args, per); break;
         case 13: echo_round_kernel<false, false, kUR, true, true, 4><<<gg, bb, 0, s>>>(args, per); break;
-        // 14 / 15 / 16: RS 2 -- the lean ranked streams (stream_tile_ranked2) with 6 / 8 / 4 row-loads per batch
-        case 14: echo_round_kernel<false, false, kUR, true, true, kRefSlack, 2><<<gg, bb, 0, s>>>(args, per); break;
-        case 15: echo_round_kernel<false, false, 8, true, true, kRefSlack, 2><<<gg, bb, 0, s>>>(args, per); break;
-        case 16: echo_round_kernel<false, false, 4, true, true, kRefSlack, 2><<<gg, bb, 0, s>>>(args, per); break;
-        // 17: LASTW -- no write-phase wait in the share's last round (reference mode); 18: the same in wire mode
-        case 17: echo_round_kernel<false, false, kUR, true, true, kRefSlack, 1, 1><<<gg, bb, 0, s>>>(args, per); break;
-        case 18: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, kRefSlack, 1, 1><<<gg, bb, 0, s>>>(args, per); break;
-        // 21: wire mode on 128-B windows (wire-form streams, one tile per wave per round, SLACK 0: the wire kernel of
-        // rounds 1-4 until replaced by the 64-B windows of wire_header_phase64); 22: as shipped with no option bit but VLAN;
-        // 23: as shipped with SLACK 0
-        case 21: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0, 1, 0, kWireWin><<<gg, bb, 0, s>>>(args, per); break;
+        // (14-16, RS 2 -- the lean ranked streams, stream_tile_ranked2 -- with 6 / 8 / 4 row-loads per batch: c4 177.9 /
+        // 179.5 / 180.8 vs 177.4 us, profiles/r04/ab/; 17 / 18, LASTW -- no write-phase wait in a share's last round: c3
+        // +1.1 us, c4 +3.0; 21, wire mode on 128-B windows, the wire kernel of rounds 1-4: c2 70.7 vs 44.0 us, c3 297.8 vs
+        // 279.7, profiles/r04/wire64/; 24, wire mode without paired short tiles: c2 44.5 vs 43.4, c3 284.4 vs 277.8,
+        // profiles/r04/wpair/.  Removed from the product header in round 5, with the 128-B wire_header_phase)
+        // 22: wire mode as shipped with no option bit but VLAN; 23: wire mode with SLACK 0
         case 22: args.opts = XSK_GPU_OPT_VLAN; echo_round_kernel<true, false><<<gg, bb, 0, s>>>(args, per); break;
         case 23: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, 0><<<gg, bb, 0, s>>>(args, per); break;
-        // 24: wire mode on 64-B windows without paired short tiles (WPAIR 0: the wire kernel before round 4's second session)
-        case 24: args.opts = XSK_GPU_OPT_ALL; wire_unpaired_kernel<<<gg, bb, 0, s>>>(args, per); break;
         // (25, one tile per wave per round -- four rounds per 1 M-frame share, a quarter of the windows in the last write
         // phase: c2 35.9 vs 35.3 us, p98 63.5 vs 63.8, c3 287.5 vs 276.4; profiles/r04/tpw1/, removed)
         // (26, REREAD -- the share's second-to-last round stores records and verdicts but not its windows, which are read

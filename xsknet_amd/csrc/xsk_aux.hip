@@ -133,18 +133,28 @@ __global__ __launch_bounds__(256) void pack_headers_kernel(const uint8_t* umem, 
     for (uint32_t k = 0; k < w; ++k) q[k] = p[k];
 }
 
-// Staged host mode, scattered descriptors: copy every frame's read span from the mapped host UMEM (across PCIe) into
-// the device mirror at the same offset.  One 16-lane row per frame (4 frames per wave), 256-B row-loads, four in
-// flight per lane before the stores -- a batch's PCIe reads overlap like the zerocopy kernel's.  Only the bytes the
-// transform will read move (xsk_gpu__read_span), never the gaps between frames.
-__global__ __launch_bounds__(256) void stage_gather_kernel(const uint8_t* src, uint8_t* dst, uint64_t umem_size,
-                                                           const xsk_gpu_desc* descs, uint32_t n, uint32_t wire) {
+// Staged host mode, scattered descriptors: copy every frame's read span into the device mirror at the same offset.
+// One 16-lane row per frame (4 frames per wave), 256-B row-loads, four in flight per lane before the stores -- a batch's
+// PCIe reads overlap like the zerocopy kernel's.  Only the bytes the transform will read move (xsk_gpu__read_span),
+// never the gaps between frames.  Two sources:
+//   offs == nullptr: the mapped host UMEM (its device alias), read across PCIe at the frame's own offset (the gather);
+//   offs != nullptr: a device staging buffer the host packed the spans into (no alias on this device): frame f's span
+//                    starts at src + offs[f]; offs[f] == UINT32_MAX marks a frame the host copied by itself.
+__global__ __launch_bounds__(256) void stage_gather_kernel(const uint8_t* src, const uint32_t* offs, uint8_t* dst,
+                                                           uint64_t umem_size, const xsk_gpu_desc* descs, uint32_t n,
+                                                           uint32_t wire) {
     const uint32_t f = (blockIdx.x * 256u + threadIdx.x) >> 4, k = threadIdx.x & 15u;
     if (f >= n) return;
     const xsk_gpu_desc d = descs[f];
     uint64_t a16 = 0;
     const uint64_t span = xsk_gpu__read_span(d.addr, d.len, umem_size, (int)wire, &a16);
-    const u32x4* s = (const u32x4*)(src + a16);
+    uint64_t from = a16;
+    if (offs) {
+        const uint32_t o = offs[f];
+        if (o == UINT32_MAX) return;
+        from = o;
+    }
+    const u32x4* s = (const u32x4*)(src + from);
     u32x4* t = (u32x4*)(dst + a16);
     const uint64_t nv = span >> 4;  // 16-B vectors
     for (uint64_t v0 = 0; v0 < nv; v0 += 64u) {
@@ -305,19 +315,31 @@ int xsk_gpu__pack_headers_dev(const void* d_umem, const struct xsk_gpu_desc* d_d
     return 0;
 }
 
-int xsk_gpu__stage_gather_dev(const void* m_umem, void* d_mirror, uint64_t umem_size, const struct xsk_gpu_desc* d_descs,
-                              uint32_t n, uint32_t wire, void* stream) {
+static int stage_gather_launch(const void* src, const uint32_t* d_offs, void* d_mirror, uint64_t umem_size,
+                               const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t wire, void* stream) {
     if (n == 0) return 0;
-    if (n > XSK_GPU_MAX_BATCH || !m_umem || !d_mirror || !d_descs) return -EINVAL;
+    if (n > XSK_GPU_MAX_BATCH || !src || !d_mirror || !d_descs) return -EINVAL;
     // <= 2^24 frames (2^22 workgroups) per launch
     constexpr uint32_t kChunk = 1u << 24;
     for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
         const uint32_t m = n - c0 < kChunk ? n - c0 : kChunk;
         hipLaunchKernelGGL(stage_gather_kernel, dim3((m + 15u) / 16u), dim3(256), 0, (hipStream_t)stream,
-                           (const uint8_t*)m_umem, (uint8_t*)d_mirror, umem_size, d_descs + c0, m, wire);
+                           (const uint8_t*)src, d_offs ? d_offs + c0 : nullptr, (uint8_t*)d_mirror, umem_size,
+                           d_descs + c0, m, wire);
         HIP_TRY(hipGetLastError());
     }
     return 0;
+}
+
+int xsk_gpu__stage_gather_dev(const void* m_umem, void* d_mirror, uint64_t umem_size, const struct xsk_gpu_desc* d_descs,
+                              uint32_t n, uint32_t wire, void* stream) {
+    return stage_gather_launch(m_umem, nullptr, d_mirror, umem_size, d_descs, n, wire, stream);
+}
+
+int xsk_gpu__stage_unpack_dev(const void* d_stage, const uint32_t* d_offs, void* d_mirror, uint64_t umem_size,
+                              const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t wire, void* stream) {
+    if (!d_offs) return -EINVAL;
+    return stage_gather_launch(d_stage, d_offs, d_mirror, umem_size, d_descs, n, wire, stream);
 }
 
 int xsk_gpu_stream_read_dev(const void* d_src, uint64_t bytes, uint64_t* d_out, void* stream) {

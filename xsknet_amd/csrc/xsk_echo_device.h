@@ -1,7 +1,8 @@
 // xsk_echo_device.h — device code of the gfx950 (MI355X / CDNA4) ICMP-echo transform: the round kernel
 // the product launches (xsk_echo.hip) and whose body the low-latency resident kernel runs (xsk_lowlat.hip).
-// Only the shipped parameter set lives here; every alternative measured in rounds 1-2 is in the tuning
-// laboratory tune/xsk_echo_lab.h (never compiled into libxsknet_amd.so).
+// Only the shipped parameter set and the switches an in-process A/B still needs live here (tune/xsk_tune_product.hip
+// instantiates those for tools/abbench.py); the alternatives measured and lost in rounds 1-4 are recorded with their A/B
+// logs in DESIGN.md §4 and in git history.
 //
 // Replaces, for a whole batch of AF_XDP descriptors at once, the per-frame call
 //   process_packet()   /root/reference/src/lib/xsk_receive.c:113-190   (gates, field swap, type 8->0,
@@ -17,8 +18,7 @@ namespace xskgpu {
 namespace {
 
 constexpr int kTile = XSK_GPU_TILE_FRAMES;  // frames per wave tile (= RX_BATCH_SIZE, xsk_utils.h:8)
-constexpr int kWin = 64;                    // reference-mode header window [a16, a16 + 64)
-constexpr int kWireWin = 128;               // wire-mode header window
+constexpr int kWin = 64;                    // header window [a16, a16 + 64), reference and wire mode
 constexpr uint32_t kMaxLen = 1u << 30;      // build-added descriptor sanity bound (XSK_GPU_MAX_LEN)
 constexpr int kWaves6 = 16;                 // waves per workgroup (one workgroup per CU)
 constexpr int kThreads6 = kWaves6 * 64;     // 1024
@@ -26,8 +26,7 @@ constexpr int kU = 4;                       // 256-B row-loads in flight per lan
 constexpr int kUR = 6;                      // the same for the launched kernel's ranked (ragged-tile) streams:
                                             // c4 185.4 -> 182.6 us, c3 / p98 unchanged (profiles/r03/ab_ranked_u6_u8_*)
 constexpr int kRefTPW = 2;                  // reference mode: tiles per wave per round (2048 frames per CU)
-constexpr int kRefHeavy = 512;              // reference mode: SYNC 2's heavy-frame threshold (bytes)
-constexpr int kWireHeavy = 1024;            // wire mode: the same
+constexpr int kRefHeavy = 512;              // SYNC 2's heavy-frame threshold (bytes)
 constexpr int kRefSlack = 2;                // reference mode: a heavy wave writes once all but 2 waves have read the
                                             // round (SLACK): c4 181.4 -> 176.5 us, c3 274.0 -> 272.9 in-process A/B
                                             // (profiles/r03/ab_slack_confirm_*.log)
@@ -209,20 +208,19 @@ __device__ __forceinline__ uint64_t meta6_a16(const FrameMeta6& m) {
 }
 
 // One frame's row stream: row-loads j = 0 .. ns-1 (lane k takes row bytes [256 j + 16 k, +16)).  The
-// first row-load carries the window: lanes 0-3 (wire: 0-7) drop it into the frame's LDS row and every lane
-// sums its bytes by exact range (ICMP [off+34, rowhi), IPv4 header [off+14, iphi)); later blocks only
-// need the frame-end mask.  WIRE: the stream sums only row bytes [128, rowhi) -- the parse, and so the ICMP
-// start and end, are known only in the header phase, which sums the in-window part from LDS.
-template <int U, class L, bool WIRE, bool D2>
+// first row-load carries the window: lanes 0-3 drop it into the frame's LDS row and every lane sums its
+// bytes by exact range (ICMP [off+34, rowhi), IPv4 header [off+14, iphi)); later blocks only need the
+// frame-end mask.
+template <int U, class L, bool D2>
 __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t f_rowhi, uint32_t f_lim,
                                              uint32_t f_off, uint32_t f_iphi, uint32_t k, uint8_t* hdr_row,
                                              RowSums& rs) {
-    const int ic_lo = WIRE ? kWireWin : (int)f_off + 34;
+    const int ic_lo = (int)f_off + 34;
     if (ns == 1u) {
         const uint32_t ro = 16u * k;
         const u32x4 x = ld.load(ro, ro < f_lim);
-        if (k < (WIRE ? 8u : 4u)) *(u32x4*)(hdr_row + ro) = x;
-        if (!WIRE) rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
+        if (k < 4u) *(u32x4*)(hdr_row + ro) = x;
+        rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
         rs.ic += sum_range(x, (int)ro, ic_lo, (int)f_rowhi);
         return;
     }
@@ -239,8 +237,8 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
             const uint32_t ro = 256u * (j0 + (uint32_t)u) + 16u * k;
             const u32x4 x = v[u];
             if (u == 0 && j0 == 0u) {
-                if (k < (WIRE ? 8u : 4u)) *(u32x4*)(hdr_row + ro) = x;
-                if (!WIRE) rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
+                if (k < 4u) *(u32x4*)(hdr_row + ro) = x;
+                rs.ip += k < 4u ? sum_range(x, (int)ro, (int)f_off + 14, (int)f_iphi) : 0ull;
                 rs.ic += sum_range(x, (int)ro, ic_lo, (int)f_rowhi);
             } else {
                 const int nb = (int)(f_rowhi - min(ro, f_rowhi));      // frame bytes in this block
@@ -268,13 +266,13 @@ __device__ __forceinline__ void stream_frame(const L& ld, uint32_t ns, uint32_t 
 // frames of a step need about the same number of row-loads (ragged batches waste fewer lanes), and each
 // batch of U row-loads is packed across consecutive steps by a wave-uniform cursor (short frames share
 // one round trip instead of paying one per step).  The IPv4 header sum is taken in the header phase from
-// the LDS window.  SKM (reference mode): tiles of frames <= 7 row-loads are ranked by counting (one
-// ballot per value), and blocks past row 0 are masked only where one of the slot's frames ends.
-template <int U, bool FAST, bool WIRE, bool SKM, bool PRIO = false>
+// the LDS window.  SKM: tiles of frames <= 7 row-loads are ranked by counting (one ballot per value), and
+// blocks past row 0 are masked only where one of the slot's frames ends.
+template <int U, bool FAST, bool SKM, bool PRIO = false>
 __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_buffer_rsrc_t rsrc,
                                                    const FrameMeta6* meta, uint32_t* sort, uint8_t* rows,
                                                    uint32_t* sums_ic, uint32_t nit_own, uint32_t lane) {
-    constexpr uint32_t kRowW = WIRE ? (uint32_t)kWireWin : (uint32_t)kWin;  // LDS row (window) bytes
+    constexpr uint32_t kRowW = (uint32_t)kWin;  // LDS row (window) bytes
     const uint32_t q = lane >> 4, k = lane & 15u;
     uint32_t rank = 0;
     if (SKM && __ballot(nit_own > 7u) == 0ull) {
@@ -367,7 +365,7 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
             const u32x4 x = v[u];
             if (uj[u] == 0u) {
                 if (k < kRowW / 16u && ulim[u]) *(u32x4*)(rows + uf[u] * kRowW + ro) = x;  // the header window
-                ic += sum_range(x, (int)ro, WIRE ? kWireWin : (int)uoff[u] + 34, (int)urowhi[u]);
+                ic += sum_range(x, (int)ro, (int)uoff[u] + 34, (int)urowhi[u]);
             } else {
                 const int nb = (int)(urowhi[u] - min(ro, urowhi[u]));
                 u32x4 y = x;
@@ -389,133 +387,18 @@ __device__ __forceinline__ void stream_tile_sorted(const EchoArgs& a, __amdgpu_b
     }
 }
 
-// Ranked streams, lean form (RS 2; the tile's frames within a 2 GiB buffer window and <= 64 KiB).  The same schedule as
-// stream_tile_sorted -- frames ranked by row-load count, step s = ranks 4s..4s+3, U row-loads per batch packed across
-// steps -- at a fraction of its instructions per row-load (round 3 counted ~300 to issue a batch of six: a readlane and
-// a dozen scalar ops per slot, and per new step two DEPENDENT LDS reads, rank -> frame -> metadata, before the step's
-// address):
-//   - each lane writes its frame's metadata to the slot of its RANK (meta[] is overwritten in rank order; the 16-B
-//     entry carries the frame's own index for the window and the sum), so a step's row reads ONE broadcast entry;
-//   - the batch's entries are read together, one LDS wait per batch, before any address work;
-//   - the slot cursor keeps the current step's row-load count in a scalar (a readlane only when a step begins);
-//   - sums are 32-bit sums of 16-bit halves (v_dot2_u32_u16, no 64-bit carries, no fold), masked only in the block a
-//     frame ends in and in row-load 0 (the window and the ICMP start).
-// The frame-of-rank index and the step row-load counts use the sort row as stream_tile_sorted does.
-template <int U, bool PRIO>
-__device__ __forceinline__ void stream_tile_ranked2(__amdgpu_buffer_rsrc_t rsrc, FrameMeta6* meta, uint32_t* sort,
-                                                    uint8_t* rows, uint32_t* sums_ic, uint32_t nit_own, uint32_t rel_own,
-                                                    uint32_t rowhi_own, uint32_t lim_own, uint32_t off_own,
-                                                    uint32_t lane) {
-    const uint32_t q = lane >> 4, k = lane & 15u;
-    uint32_t rank = 0;
-    if (__ballot(nit_own > 7u) == 0ull) {  // counting rank (one ballot per value), as stream_tile_sorted
-        uint32_t below = 0;
-#pragma unroll
-        for (uint32_t v = 0; v < 8u; ++v) {
-            const uint64_t bv = __ballot(nit_own == v);
-            const uint32_t mb = __builtin_amdgcn_mbcnt_hi((uint32_t)(bv >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bv, 0u));
-            if (nit_own == v) rank = below + mb;
-            below += (uint32_t)__popcll(bv);
-        }
-    } else {
-        for (uint32_t j = 0; j < 64u; ++j) {
-            const uint32_t nj = rdlane(nit_own, j);
-            rank += (nj < nit_own || (nj == nit_own && j < lane)) ? 1u : 0u;
-        }
-    }
-    // the tile's metadata in rank order (lane = frame wrote meta[lane] before; every lane rewrites one entry, a
-    // permutation, in one wave instruction) -- .packed = off | frame << 8
-    {
-        FrameMeta6 m;
-        m.rel = rel_own;
-        m.rowhi = rowhi_own;
-        m.lim = lim_own;
-        m.packed = off_own | (lane << 8);
-        meta[rank] = m;
-    }
-    if ((rank & 3u) == 3u) sort[64u + (rank >> 2)] = nit_own;  // sort[64 + s]: row-loads of step s
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t stepns = sort[64u + (lane & 15u)];  // lane s (< 16): row-loads of step s
-    uint32_t s = 0;
-    while (s < 16u && rdlane(stepns, s) == 0u) ++s;
-    uint32_t ns = s < 16u ? rdlane(stepns, s) : 0u, j = 0;  // the cursor: step s, its row-loads, row-load j
-    uint32_t cur = 16u, cur_f = 0u, h = 0u;                   // the step being summed, its frame (per row), sum
-    while (s < 16u) {
-        uint32_t us[U], uj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // wave-uniform slot assignment
-            us[u] = s;
-            uj[u] = j;
-            if (s < 16u && ++j >= ns) {
-                ++s;
-                j = 0;
-                ns = s < 16u ? rdlane(stepns, s) : 0u;
-            }
-        }
-        FrameMeta6 fm[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)  // every slot's entry (slots of one step read the same one: a broadcast)
-            if (us[u] < 16u) fm[u] = meta[4u * us[u] + q];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        u32x4 v[U];
-        if (PRIO) __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            v[u] = u32x4{0u, 0u, 0u, 0u};
-            if (us[u] < 16u) {
-                const uint32_t ro = 256u * uj[u] + 16u * k;
-                v[u] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(ro < fm[u].lim ? fm[u].rel + ro : 0x80000000u), 0,
-                                                             kAuxNT);
-            }
-        }
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (us[u] >= 16u) continue;  // uniform
-            if (us[u] != cur) {          // uniform: a new step begins in this slot
-                if (cur < 16u) {
-                    const uint32_t r = row_sum_dpp(h);
-                    if (k == 15u) sums_ic[cur_f] = r;
-                }
-                cur = us[u];
-                cur_f = fm[u].packed >> 8;
-                h = 0u;
-            }
-            const uint32_t ro = 256u * uj[u] + 16u * k;
-            u32x4 x = v[u];
-            const int hi = (int)fm[u].rowhi;
-            if (uj[u] == 0u) {
-                if (k < 4u && fm[u].lim) *(u32x4*)(rows + cur_f * (uint32_t)kWin + ro) = x;  // the header window
-                x &= range_mask((int)ro, (int)(fm[u].packed & 0xFFu) + 34, hi);
-            } else if (__ballot((int)ro < hi && hi < (int)ro + 16) != 0ull) {  // a block some row's frame ends in
-                const int nb = hi - (int)min(ro, (uint32_t)hi);
-                x.x &= dw_mask(nb);
-                x.y &= dw_mask(nb - 4);
-                x.z &= dw_mask(nb - 8);
-                x.w &= dw_mask(nb - 12);
-            }
-            h = sum_halves(x, h);
-        }
-    }
-    if (cur < 16u) {
-        const uint32_t r = row_sum_dpp(h);
-        if (k == 15u) sums_ic[cur_f] = r;
-    }
-}
-
 // Uniform long tiles: every frame of the tile parsed, at the same 16-B offset and with the same end, so
 // the ICMP byte range [lo, hi) = [off + 34, off + len) is the same in every row.  A lane's byte masks are
 // then the same for every step: computed once per tile for the first and the last row-load (the only blocks
 // the range can cut; the others are whole or, past `lim`, not loaded), and a step costs its loads, one
 // v_dot2_u32_u16 per dword, two masks and the row reduction.  The sums are plain 32-bit sums of 16-bit halves
 // (< 2^32 for frames <= 64 KiB: 257 blocks x 8 halves x 65535 x 16 lanes); the IPv4 header sum comes from the
-// window in the header phase.  WIRE: 128-B windows, and the stream sums row bytes [128, rowhi) (lo = 128).
-template <int U, bool WIRE, bool SPLIT = false, bool PRIO = false>
+// window in the header phase.
+template <int U, bool SPLIT = false, bool PRIO = false>
 __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc, const FrameMeta6* meta, uint8_t* rows,
                                                     uint32_t* sums_ic, uint32_t ns, uint32_t lo, uint32_t hi,
                                                     uint32_t lane) {
-    constexpr uint32_t kRowW = WIRE ? (uint32_t)kWireWin : (uint32_t)kWin;
+    constexpr uint32_t kRowW = (uint32_t)kWin;
     const uint32_t q = lane >> 4, k = lane & 15u;
     const u32x4 mf = range_mask((int)(16u * k), (int)lo, (int)hi);                    // row-load 0
     const u32x4 ml = range_mask((int)(256u * (ns - 1u) + 16u * k), (int)lo, (int)hi);  // row-load ns - 1
@@ -677,14 +560,9 @@ __device__ __forceinline__ bool header_phase_ref(const EchoArgs& a, uint8_t* row
 
 // ================================================================================================
 // Wire-format header phase (xsk_gpu_echo_dev_opts; spec: include/xsk_gpu.h).
-// Lane = frame.  `row` is the frame's 16-B aligned 128-B window in LDS (frame byte i at row[off + i]),
-// `far_raw` the stream's folded sum of row bytes [128, off + len) (absolute-alignment domain).  Parses
-// VLAN tags / IHL / tot_len / fragments, sums the IPv4 header and the in-window part of the ICMP message
-// from LDS, completes the message sum (re-reading [128, off + end) from memory in the rare case that
-// STRICT cuts a message short of the frame beyond the window), decides, patches the reply in LDS.
-// Returns true when the patched 64-B window should leave as a whole sector (aligned, rewrite < 64 B).
 // ================================================================================================
-// Tag types for the two instantiations of the IPv4 gates of the wire header phases (untagged frame: every field at a constant offset).
+// Tag types for the two instantiations of the IPv4 gates of the wire header phase (untagged frame: every field at a
+// constant offset).
 struct WireAt14 {
     static constexpr bool kPlain = true;
 };
@@ -692,217 +570,13 @@ struct WireAtL3 {
     static constexpr bool kPlain = false;
 };
 
-__device__ __forceinline__ uint32_t wbe16(const uint8_t* p, uint32_t i) {
-    return ((uint32_t)p[i] << 8) | (uint32_t)p[i + 1];
-}
-
-__device__ __forceinline__ bool wire_header_phase(const EchoArgs& a, uint8_t* row, uint32_t far_raw, uint64_t addr,
-                                                  uint32_t len, bool ok, bool live, uint32_t wend, Counters& cnt,
-                                                  u32x4* rec_out, uint32_t* verd_out) {
-    const bool strict = (a.opts & XSK_GPU_OPT_STRICT_IPV4) != 0u;
-    const bool vlan = (a.opts & XSK_GPU_OPT_VLAN) != 0u;
-    const bool verify = (a.opts & XSK_GPU_OPT_VERIFY_CSUM) != 0u;
-    const uint32_t off = (uint32_t)addr & 15u;
-    uint8_t* p = row + off;  // frame byte i = p[i] for off + i < wend
-    // the frame's first 40 bytes as frame-relative LE dwords: an untagged frame's fields at constant offsets come from
-    // registers instead of one LDS byte read each (as wire_header_phase64)
-    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
-    uint32_t h[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
-    auto hb = [&](uint32_t i) -> uint32_t { return (h[i >> 2] >> (8u * (i & 3u))) & 0xFFu; };  // i < 40, constant
-    auto hbe16 = [&](uint32_t i) -> uint32_t { return (hb(i) << 8) | hb(i + 1u); };
-    uint32_t verdict = XSK_GPU_TX_REPLY;
-    uint32_t l3 = 14, hl = 20, end = len, et = 0, tags = 0;
-    bool hdrs = false;  // all three headers inside the frame: the record is filled
-    auto ipv4_gates = [&](auto at) {  // after the tags (untagged: l3 = 14, every byte from h[])
-        constexpr bool PL = decltype(at)::kPlain;
-        auto B = [&](uint32_t k) -> uint32_t { return PL ? hb(14u + k) : (uint32_t)p[l3 + k]; };
-        auto BE = [&](uint32_t k) -> uint32_t { return PL ? hbe16(14u + k) : wbe16(p, l3 + k); };
-        bool bad = false;
-        if (strict) {
-            const uint32_t vihl = B(0);
-            if ((vihl >> 4) != 4u || (vihl & 15u) < 5u) bad = true;
-            else {
-                hl = 4u * (vihl & 15u);
-                const uint32_t tot = BE(2);
-                if (tot < hl + 8 || l3 + tot > len) bad = true;
-                else if (BE(6) & 0x3FFFu) bad = true;
-                else end = l3 + tot;
-            }
-        }
-        if (bad) verdict = XSK_GPU_DROP_BAD_IP;
-        else if (B(9) != 1u) verdict = XSK_GPU_DROP_NOT_ICMP;
-        else if (len < l3 + hl + 8) verdict = XSK_GPU_DROP_SHORT;
-        else hdrs = true;
-    };
-    if (!ok) verdict = XSK_GPU_DROP_BAD_DESC;
-    else if (len < 14) verdict = XSK_GPU_DROP_SHORT;
-    else {
-        et = hbe16(12);
-        bool cut = false;
-        if (vlan) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                if (!cut && (et == 0x8100u || et == 0x88A8u) && tags == (uint32_t)g) {
-                    if (len < l3 + 4) cut = true;
-                    else {
-                        et = wbe16(p, l3 + 2);
-                        l3 += 4;
-                        tags++;
-                    }
-                }
-            }
-        }
-        if (cut) verdict = XSK_GPU_DROP_SHORT;
-        else if (et != 0x0800u) verdict = XSK_GPU_DROP_NOT_IPV4;
-        else if (len < l3 + 20) verdict = XSK_GPU_DROP_SHORT;
-        else if (tags == 0u) ipv4_gates(WireAt14{});
-        else ipv4_gates(WireAtL3{});
-    }
-    const uint32_t l4 = l3 + hl;
-    const bool std34 = tags == 0u && hl == 20u;  // l3 = 14, l4 = 34: the reference's offsets
-    uint32_t ip_sum = 0, ic_sum = 0, itype = 0, icode = 0, csum_in = 0, flags = 0;
-    if (hdrs) {
-        // in-window sums (absolute-alignment domain: LE dwords of the 16-B aligned row), 16 B per LDS read
-        const uint32_t ic_end = off + end, ic_hi_w = min(ic_end, (uint32_t)kWireWin);
-        uint64_t ip_acc = 0, ic_acc = 0;
-#pragma unroll
-        for (int b = 0; b < (int)kWireWin / 16; ++b) {
-            const u32x4 x = ((const u32x4*)row)[b];
-            if (!std34) ip_acc += sum_range(x, 16 * b, (int)(off + l3), (int)(off + l4));
-            ic_acc += sum_range(x, 16 * b, (int)(off + l4), (int)ic_hi_w);
-        }
-        if (std34) {  // the IPv4 header [14, 34) from the frame-relative dwords (as header_phase_ref)
-            ip_acc = dot2_halves(h[3] >> 16, dot2_halves(h[4], dot2_halves(h[5], 0u)));
-            ip_acc = dot2_halves(h[8] & 0xFFFFu, dot2_halves(h[7], dot2_halves(h[6], (uint32_t)ip_acc)));
-        }
-        uint64_t far = 0;
-        if (ic_end > (uint32_t)kWireWin) {
-            if (end == len) {
-                far = far_raw;  // the stream summed exactly [128, off + len)
-            } else {            // STRICT message ending before the frame does, beyond the window: re-read
-                const uint8_t* fb = a.umem + (addr & ~15ull);
-                for (uint32_t o = kWireWin; o < ic_end; o += 4u)
-                    far += keep_bytes(*(const uint32_t*)(fb + o), (int)o, kWireWin, (int)ic_end);
-            }
-        }
-        if (std34) {  // frame-relative halves: byte-swapped network words (RFC 1071 §2(B)), as header_phase_ref
-            ip_sum = bswap16(fold32((uint32_t)ip_acc));
-            ic_sum = fold64(ic_acc + far);
-            if (!((uint32_t)addr & 1u)) ic_sum = bswap16(ic_sum);
-        } else {
-            ip_sum = fold64(ip_acc);
-            ic_sum = fold64(ic_acc + far);
-            if (!((uint32_t)addr & 1u)) {
-                ip_sum = bswap16(ip_sum);
-                ic_sum = bswap16(ic_sum);
-            }
-        }
-        itype = std34 ? hb(34) : p[l4];
-        icode = std34 ? hb(35) : p[l4 + 1];
-        csum_in = std34 ? hbe16(36) : wbe16(p, l4 + 2);
-        if (ip_sum == 0xFFFFu) flags |= XSK_GPU_F_IP_CSUM_OK;
-        if (ic_sum == 0xFFFFu) flags |= XSK_GPU_F_ICMP_CSUM_OK;
-        if (tags) flags |= XSK_GPU_F_VLAN;
-        if (hl > 20u) flags |= XSK_GPU_F_IP_OPTIONS;
-        if (itype != 8u || (strict && icode != 0u)) verdict = XSK_GPU_DROP_NOT_ECHO;
-        else if (verify && (ip_sum != 0xFFFFu || ic_sum != 0xFFFFu)) verdict = XSK_GPU_DROP_BAD_CSUM;
-    }
-    const bool tx = hdrs && verdict == XSK_GPU_TX_REPLY;
-    uint32_t csum_out = csum_in;
-    bool wb = false;
-    if (tx) {
-        // csum_replace2(&icmp->checksum, ICMP_ECHO, ICMP_ECHOREPLY) on the LE-loaded field (xsk_receive.c:101-111)
-        const uint32_t csum_le = ((csum_in & 0xFFu) << 8) | (csum_in >> 8);
-        uint32_t c16 = (~csum_le) & 0xFFFFu;
-        c16 = (c16 + 0xFFF7u) & 0xFFFFu;
-        c16 += c16 < 0xFFF7u ? 1u : 0u;
-        const uint32_t csum_new_le = (~c16) & 0xFFFFu;
-        csum_out = bswap16(csum_new_le);
-        if (std34) {
-            // the reference's offsets: the rewrite of xsk_receive.c:148-157 as header_phase_ref's dword shuffles
-            const uint32_t n0 = (h[1] >> 16) | (h[2] << 16);              // s0 s1 s2 s3
-            const uint32_t n1 = (h[2] >> 16) | (h[0] << 16);              // s4 s5 d0 d1
-            const uint32_t n2 = (h[0] >> 16) | (h[1] << 16);              // d2 d3 d4 d5
-            const uint32_t n6 = (h[6] & 0xFFFFu) | (h[7] & 0xFFFF0000u);  // csum(ip) | daddr[0:2]
-            const uint32_t n7 = (h[8] & 0xFFFFu) | (h[6] & 0xFFFF0000u);  // daddr[2:4] | saddr[0:2]
-            const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
-            if (off == 0u && wend >= 64u) {
-                uint32_t* r32 = (uint32_t*)row;  // patched in LDS, stored as a whole 64-B sector in the write phase
-                r32[0] = n0;
-                r32[1] = n1;
-                r32[2] = n2;
-                r32[6] = n6;
-                r32[7] = n7;
-                r32[8] = n8;
-                r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
-                wb = true;
-            } else {  // byte-exact: only the rewritten bytes
-                uint8_t* pkt = a.umem + addr;
-                const uint32_t w[6] = {n0, n1, n2, n6, n7, n8};
-#pragma unroll
-                for (int b = 0; b < 12; ++b) pkt[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-#pragma unroll
-                for (int b = 26; b < 35; ++b) pkt[b] = (uint8_t)(w[3 + ((b - 24) >> 2)] >> (8 * (b & 3)));
-                pkt[36] = (uint8_t)csum_new_le;
-                pkt[37] = (uint8_t)(csum_new_le >> 8);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {  // xsk_receive.c:148-157 at the parsed offsets, in LDS
-                const uint8_t x = p[i];
-                p[i] = p[6 + i];
-                p[6 + i] = x;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint8_t x = p[l3 + 12 + i];
-                p[l3 + 12 + i] = p[l3 + 16 + i];
-                p[l3 + 16 + i] = x;
-            }
-            p[l4] = 0;
-            p[l4 + 2] = (uint8_t)csum_new_le;
-            p[l4 + 3] = (uint8_t)(csum_new_le >> 8);
-            if (off == 0u && l4 + 4u <= 64u && wend >= 64u) {
-                wb = true;  // whole 64-B sector, stored in the write phase
-            } else {        // byte-exact: only the rewritten bytes
-                uint8_t* pkt = a.umem + addr;
-#pragma unroll
-                for (int i = 0; i < 12; ++i) pkt[i] = p[i];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) pkt[l3 + 12 + i] = p[l3 + 12 + i];
-                pkt[l4] = 0;
-                pkt[l4 + 2] = p[l4 + 2];
-                pkt[l4 + 3] = p[l4 + 3];
-            }
-        }
-    }
-    const uint32_t vihl = hdrs ? (tags == 0u ? hb(14) : (uint32_t)p[l3]) : 0u, proto = hdrs ? 1u : 0u;
-    u32x4 r;
-    r.x = verdict | (flags << 8) | (proto << 16) | (itype << 24);
-    r.y = icode | (vihl << 8) | ((hdrs ? et : 0u) << 16);
-    r.z = csum_in | (csum_out << 16);
-    r.w = ip_sum | (ic_sum << 16);
-    *rec_out = r;
-    *verd_out = verdict;
-    if (live) {
-        cnt.rxp += 1;
-        cnt.rxb += len;
-        if (tx) {
-            cnt.txp += 1;
-            cnt.txb += len;
-        }
-    }
-    return wb;
-}
-
-// Wire-format header phase on the reference-form stream (WW 64): the frame's 16-B aligned 64-B window in LDS
-// (`row`, frame byte i at row[off + i] while off + i < 64; bytes past it -- an ICMP header behind two VLAN tags and
-// IPv4 options -- are read from the UMEM) and the stream's ICMP sum of row bytes [off + 34, off + len), i.e. of the
-// message of a PLAIN frame (no tag, IHL 5, no Ethernet padding under STRICT).  Same spec, verdicts, records and
-// rewrite as wire_header_phase; a plain frame's sums come from the window and the stream exactly as in reference
-// mode, any other frame's from a re-read of its header and message bytes (rare traffic, per lane).
+// Lane = frame.  The frame's 16-B aligned 64-B window in LDS (`row`, frame byte i at row[off + i] while off + i < 64;
+// bytes past it -- an ICMP header behind two VLAN tags and IPv4 options -- are read from the UMEM) and the stream's
+// ICMP sum of row bytes [off + 34, off + len), i.e. of the message of a PLAIN frame (no tag, IHL 5, no Ethernet
+// padding under STRICT).  Parses VLAN tags / IHL / tot_len / fragments, decides, patches the reply in LDS; a plain
+// frame's sums come from the window and the stream exactly as in reference mode, any other frame's from a re-read of
+// its header and message bytes (rare traffic, per lane).  Returns true when the patched 64-B window should leave as a
+// whole sector (aligned, rewrite inside the first 64 B).
 __device__ __forceinline__ uint64_t sum_row_range(const uint8_t* rb, uint32_t lo, uint32_t hi) {
     uint64_t acc = 0;  // LE dwords of the 16-B aligned row at rb, bytes [lo, hi) (absolute-alignment domain)
     for (uint32_t o = lo & ~3u; o < hi; o += 4u) acc += keep_bytes(*(const uint32_t*)(rb + o), (int)o, (int)lo, (int)hi);
@@ -1098,12 +772,11 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
     return wb;
 }
 
-// LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB in reference mode): TPW header-window
-// tiles per wave, the per-frame metadata and sums, the ranked streams' sort rows, the counter rows.
-template <int TPW, bool WIRE>
+// LDS of one round-kernel workgroup (152.5 KiB of the CU's 160 KiB): TPW header-window tiles per wave, the
+// per-frame metadata and sums, the ranked streams' sort rows, the counter rows.
+template <int TPW>
 struct Echo6Smem {
-    static constexpr uint32_t kRowW = WIRE ? (uint32_t)kWireWin : (uint32_t)kWin;
-    __attribute__((aligned(16))) uint8_t hdr[kWaves6][TPW][kTile * kRowW];  // 128 KiB: header windows
+    __attribute__((aligned(16))) uint8_t hdr[kWaves6][TPW][kTile * kWin];  // 128 KiB: header windows
     __attribute__((aligned(16))) FrameMeta6 meta[kWaves6][kTile];          // 16 KiB
     uint32_t sum[kWaves6][2][kTile];                                        // 8 KiB
     uint32_t sort[kWaves6][80];                                             // 5 KiB
@@ -1233,40 +906,29 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // echo6_body: the work over the tiles [t_begin, t_end) of one workgroup (every wave of the workgroup calls
 // it with the same range); echo_round_kernel runs it once per workgroup on its static share, the
 // low-latency resident kernel (xsk_lowlat.hip) once per doorbell.
-//   TPW   tiles per wave per round (2; wire mode on 128-B windows and sub-tiles 1)
+//   TPW   tiles per wave per round (2; sub-tiles 1)
 //   SYNC  how a wave enters its write phase.  0: at once (one-round small batches); 2: a wave at least half
 //         of whose frames this round have >= HEAVY bytes waits until every wave of the workgroup but SLACK has
 //         read the round (LDS arrival counter), lighter waves go ahead -- the phase separation pays where reads
 //         dominate, and costs latency hiding where frames are short
-//   WIRE  the wire-format mode (a.opts != 0): on 64-B windows (WW, the launched kernel) the reference mode's streams
-//         and rounds with wire_header_phase64; on 128-B windows (sub-tiles, the low-latency kernel) wire-form streams
-//         and wire_header_phase
+//   WIRE  the wire-format mode (a.opts != 0): the reference mode's streams and rounds with wire_header_phase64
 //   SUBT  tiles of a.tile_live frames (small batches: the batch spreads over every wave)
 //   TRACE wave 0 stamps the body's phase boundaries into a.trace (the low-latency kernel's diagnostics)
 //   DLDS  the descriptors may already be in the LDS (a.desc_in_lds, the low-latency kernel's first poll)
 //   WT    write-phase windows and records stored write-through (sc1 raw buffer stores)
-// Reference mode adds the per-tile stream choices: tiles whose frames all fit their 64-B windows (c2)
+// The per-tile stream choices: tiles whose frames all fit their 64-B windows (c2)
 // skip the row stream (and two such tiles of a round are read together, PAIR), ping-size tiles (every frame
 // within 128 B) are read by 8-lane groups, uniform long tiles (c3, c5) take masks computed once per tile,
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0, int RS = 1, int LASTW = 0, int WW = kWireWin,
-          int WPAIR = 1>
-__device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end,
-                                           Echo6Smem<TPW, WIRE && WW != kWin>& sm) {
-    // WW: wire mode's LDS window -- 128 B (the whole parsed header in LDS, the stream summing bytes from 128 on, one
-    // tile per wave per round) or 64 B (reference-form streams and rounds, wire_header_phase64)
-    constexpr bool SW = WIRE && WW != kWin;  // wire-form streams: 128-B rows, the stream's ICMP part from byte 128
-    static_assert(!SW || TPW == 1, "wire windows of 128 B: one tile per wave per round");
-    static_assert(WW == kWin || WW == kWireWin, "wire window: 64 or 128 B");
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0>
+__device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, Echo6Smem<TPW>& sm) {
     static_assert(SYNC == 0 || SYNC == 2, "write phases: at once (0) or heavy waves wait for the round (2)");
     static_assert(SLACK >= 0 && SLACK < kWaves6, "SLACK: waves a heavy wave does not wait for");
     constexpr int U = kU;
-    constexpr bool REF = !SW;                            // reference-form stream choices (D2 / MID / SKM)
-    // paired short tiles (header_phase_ref; in wire mode on 64-B windows wire_header_phase64 unless WPAIR == 0)
-    constexpr bool PAIR = !SW && TPW == 2 && !SUBT && (!WIRE || WPAIR);
-    constexpr uint32_t kRowW = SW ? (uint32_t)kWireWin : (uint32_t)kWin;  // LDS row (header window) bytes
+    constexpr bool PAIR = TPW == 2 && !SUBT;  // paired short tiles (header_phase_ref / wire_header_phase64)
+    constexpr uint32_t kRowW = (uint32_t)kWin;  // LDS row (header window) bytes
     auto& s_hdr = sm.hdr;
     uint32_t& s_arrive = sm.arrive;
     if (SYNC == 2) {
@@ -1334,11 +996,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 const uint32_t lim = max(rowhi, win);
                 const uint32_t nit = (lim + 255u) >> 8;
                 const bool short_tile = __ballot(lim > kRowW) == 0ull;
-                const bool mid_tile = REF && !short_tile && __ballot(lim > 128u) == 0ull;
+                const bool mid_tile = !short_tile && __ballot(lim > 128u) == 0ull;
                 // every frame of the tile at the same 16-B offset with the same end (c2, pings): the ICMP
                 // byte masks of a lane's block are the same for all its frames -> computed once per tile
                 const uint32_t ukey = (off << 24) ^ rowhi;
-                const bool uni_tile = REF && (short_tile || mid_tile) && __ballot(ukey != uniform(ukey)) == 0ull;
+                const bool uni_tile = (short_tile || mid_tile) && __ballot(ukey != uniform(ukey)) == 0ull;
                 uint64_t wlo = 0, span = ~0ull;
                 if (!short_tile) {
                     wlo = wave_min_u64(nit ? a16 : ~0ull);
@@ -1364,26 +1026,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     WinLoader ld;
                     ld.r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + (fast ? wlo : 0ull)), (short)0,
                                                              fast ? (int)((span + 15u) & ~15ull) : 0, kRsrcFlags);
-                    if (SW && short_tile) {
-                        // every frame within its 128-B window: 8 lanes per frame, 8 frames per wave-load;
-                        // nothing lies past byte 128, so the streamed part of every sum is zero
-                        const uint32_t kk = lane & 7u, ro = 16u * kk;
-                        u32x4 x[8];
-#pragma unroll
-                        for (int r = 0; r < 8; ++r) {
-                            const FrameMeta6& fm = meta[(uint32_t)r * 8u + (lane >> 3)];
-                            const bool in = ro < fm.lim;
-                            x[r] = u32x4{0u, 0u, 0u, 0u};  // lanes past their frame: no memory access at all
-                            if (in) x[r] = __builtin_nontemporal_load((const u32x4*)(a.umem + meta6_a16(fm) + ro));
-                        }
-#pragma unroll
-                        for (int r = 0; r < 8; ++r) {
-                            const uint32_t f = (uint32_t)r * 8u + (lane >> 3);
-                            const u32x4 v = ro < meta[f].lim ? x[r] : u32x4{0u, 0u, 0u, 0u};
-                            *(u32x4*)(rows + f * kRowW + ro) = v;
-                        }
-                        sums_ic[lane] = 0u;
-                    } else if (short_tile) {
+                    if (short_tile) {
                         // every frame within its 64-B window: 4 lanes per frame, 16 frames per wave-load
                         const uint32_t kk = lane & 3u, ro = 16u * kk;
                         const u32x4 umk = uni_tile ? range_mask((int)ro, (int)off + 34, (int)rowhi) : u32x4{0u, 0u, 0u, 0u};
@@ -1407,7 +1050,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                             ric += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ric, 0x4E, 0xF, 0xF, false);  // xor 2
                             if (kk == 0u) sums_ic[f] = ric;
                         }
-                    } else if (REF && mid_tile) {
+                    } else if (mid_tile) {
                         // every frame within 128 B of its 16-B aligned start (pings): 8 lanes per frame, 8 frames
                         // per wave-load, all 8 loads in flight at once; the ICMP sum by exact byte range, reduced
                         // over the 8 lanes (the IPv4 header sum comes from the window in the header phase)
@@ -1437,14 +1080,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     } else if (__ballot(nit != 0u && nit != uniform(max_nit_lane(nit))) != 0ull ||
                                uniform(max_nit_lane(nit)) < (uint32_t)U) {
                         // ragged tile (or one too short to fill a batch of U row-loads): ranked streams
-                        if (RS == 2 && REF && fast && uniform(max_nit_lane(nit)) <= 257u)
-                            stream_tile_ranked2<UR, PRIO>(ld.r, meta, sm.sort[wave], rows, sums_ic, nit,
-                                                          nit ? (uint32_t)(a16 - wlo) : 0u, rowhi, lim, off, lane);
-                        else if (fast) stream_tile_sorted<UR, true, SW, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
-                        else stream_tile_sorted<UR, false, SW, REF, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        if (fast) stream_tile_sorted<UR, true, true, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
+                        else stream_tile_sorted<UR, false, true, PRIO>(a, ld.r, meta, sm.sort[wave], rows, sums_ic, nit, lane);
                     } else if (fast && __ballot(!parse) == 0ull && __ballot(ukey != uniform(ukey)) == 0ull) {
-                        stream_tile_uniform<U, SW, USPLIT, PRIO>(ld.r, meta, rows, sums_ic, uniform(nit),
-                                                     SW ? (uint32_t)kWireWin : uniform(off) + 34u, uniform(rowhi), lane);
+                        stream_tile_uniform<U, USPLIT, PRIO>(ld.r, meta, rows, sums_ic, uniform(nit), uniform(off) + 34u,
+                                                             uniform(rowhi), lane);
                     } else {
                         // every frame the same number of row-loads, but different offsets or ends: per-step streams
                         for (uint32_t s = 0; s < 16; ++s) {
@@ -1460,11 +1100,11 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                             RowSums rs;
                             if (fast) {
                                 ld.rel = fm.rel;
-                                stream_frame<U, WinLoader, SW, REF>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                                stream_frame<U, WinLoader, true>(ld, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                             } else {  // frames of one tile more than 2 GiB apart (never in AF_XDP layouts)
                                 FarLoader fl;
                                 fl.fbase = a.umem + (f_nit ? meta6_a16(fm) : 0ull);
-                                stream_frame<U, FarLoader, SW, REF>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
+                                stream_frame<U, FarLoader, true>(fl, ns, f_rowhi, f_lim, f_off, f_iphi, k, rows + f * kRowW, rs);
                             }
                             const uint32_t ric = row_sum_dpp(fold64(rs.ic));
                             if (k == 15u) sums_ic[f] = ric;
@@ -1478,10 +1118,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 __builtin_amdgcn_wave_barrier();
                 const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
                 bool wb;
-                if (WIRE && SW)
-                    wb = wire_header_phase(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
-                                           &verd_o);
-                else if (WIRE)
+                if (WIRE)
                     wb = wire_header_phase64(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
                                              &verd_o);
                 else
@@ -1503,10 +1140,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         if (SYNC == 2) {
             ++rounds_done;
             if (lane == 0) atomicAdd(&s_arrive, 1u);
-            // LASTW: in the share's last round no wave waits -- its writes have no later reads of this workgroup to
-            // stay out of the way of, and the kernel's tail is that round's write phase
-            if ((LASTW == 0 || r0 + kRound < t_end) &&
-                uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
+            if (uniform(round_long) * 2u >= (uint32_t)(kTile * TPW)) {  // at least half its frames long
                 // (every wave but SLACK: the last waves of a round are usually ragged ones still streaming)
                 while (__hip_atomic_load(&s_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
                        rounds_done * (uint32_t)kWaves6 - (uint32_t)SLACK)
@@ -1563,21 +1197,20 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 
 // The launched transform: one 16-wave workgroup per CU, each the same contiguous share of tiles_per_wg
 // tiles (echo6_geometry); reference or wire mode (WIRE), large batches or one workgroup of sub-tiles of
-// a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).  Large wire batches run on 64-B windows
-// (44 / 280 / 185 us for c2 / c3 / c4 against 71 / 298 / 215 on the 128-B windows of rounds 1-4, in-process A/B,
-// profiles/r04/wire64/).
+// a.tile_live frames (SUBT: writes as soon as a wave has read, plain stores).  Wire batches run on the same 64-B
+// windows (44 / 280 / 185 us for c2 / c3 / c4 against 71 / 298 / 215 on the 128-B windows of rounds 1-4, in-process
+// A/B, profiles/r04/wire64/).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = SUBT ? 0 : kRefSlack, int RS = 1, int LASTW = 0, int WW = WIRE ? kWin : kWireWin>
+          int SLACK = SUBT ? 0 : kRefSlack>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
-    constexpr bool SW = WIRE && WW != kWin;  // wire mode on 128-B windows
-    constexpr int TPW = (SW || SUBT) ? 1 : kRefTPW;
-    __shared__ Echo6Smem<TPW, SW> sm;
+    constexpr int TPW = SUBT ? 1 : kRefTPW;
+    __shared__ Echo6Smem<TPW> sm;
     const uint32_t tl = SUBT ? a.tile_live : (uint32_t)kTile;
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, SW ? kWireHeavy : kRefHeavy, UR, USPLIT, PRIO,
-               SLACK, RS, LASTW, WW>(a, t_begin, t_end, sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, kRefHeavy, UR, USPLIT, PRIO, SLACK>(a, t_begin, t_end,
+                                                                                                    sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.

@@ -16,14 +16,14 @@
  *   STAGED:   the bytes the transform reads are copied host->device into a device mirror of the UMEM (one
  *             strided 2-D DMA copy when the chunk has a uniform frame stride, one copy of the chunk's span when its
  *             frames cover it densely, else -- AF_XDP's recycled, scattered descriptors -- a gather kernel that
- *             moves each frame's own bytes across PCIe), transformed in HBM, and only the 38 rewritten header
- *             bytes of TX_REPLY frames are copied back and scattered into the UMEM — bytes the batch does not own
- *             are never written.  Batches of more than one chunk run as a two-stream pipeline: a copy stream
- *             takes every chunk's copy-in back to back and a compute stream each chunk's transform, header pack
- *             and copy-back once its copy-in has landed; a copy-in that may write another chunk's mirror bytes (an
- *             unaligned frame's read span reaches into its neighbour's first bytes; the dense-span copy) first waits
- *             for the previous chunk's pack.  The last chunks halve in size, and the host scatters chunk i while
- *             later chunks are still in flight.
+ *             moves each frame's own bytes across PCIe, or, on a device without a mapped alias of the UMEM, a host
+ *             pack of those bytes into pinned staging; xsk_stage_plan.h decides), transformed in HBM, and only the
+ *             38 rewritten header bytes of TX_REPLY frames are copied back and scattered into the UMEM — bytes the
+ *             batch does not own are never written.  Batches of more than one chunk run as a two-stream pipeline: a
+ *             copy stream takes every chunk's copy-in back to back and a compute stream each chunk's transform,
+ *             header pack and copy-back once its copy-in has landed; a copy-in that may write mirror bytes of an
+ *             earlier chunk's frames (xsk_stage_plan.h, `contained`) first waits for the previous chunk's pack.  The
+ *             last chunks halve in size, and the host scatters chunk i while later chunks are still in flight.
  */
 #define _GNU_SOURCE
 #define __HIP_PLATFORM_AMD__ 1
@@ -34,13 +34,14 @@
 #include <string.h>
 
 #include "xsk_gpu_internal.h"
+#include "xsk_stage_plan.h"
 
 #define NSTREAMS 2
 #define CHUNK_FRAMES 32768u /* staged pipeline granule: ~49 MB of 1500-B frames per copy-in */
 #define TAIL_FRAMES 4096u   /* staged: the last chunks halve down to this, so the work left after the last copy-in
                              * (transform, pack, copy-back, host scatter of one chunk) is short */
 #define PACK 96u            /* staged: bytes per frame of the packed rewritten headers (wire mode <= 86) */
-#define WIRE_WIN 128u       /* wire mode's header window (xsk_wire.hip) */
+#define STAGE_HALF (32u << 20) /* staged without a mapped alias: default bytes per half of the host-pack staging */
 
 struct xsk_gpu_ctx {
     int device;
@@ -69,8 +70,13 @@ struct xsk_gpu_ctx {
     hipEvent_t* done; /* [max_chunks]: chunk's results are in host memory */
     hipEvent_t* packed; /* STAGED [max_chunks]: chunk's rewritten headers are packed (its mirror bytes are free) */
     hipEvent_t* in_done; /* STAGED [max_chunks]: chunk's copy-in has landed in the mirror */
-    uint64_t staged[5]; /* STAGED: bytes copied in, chunks copied as 2-D strides / dense spans / by the gather kernel,
-                         * chunks whose copy-in was contained (not ordered after the previous chunk's pack) */
+    uint64_t staged[XSK_GPU__STAGED_STATS]; /* STAGED: the copy-in record (xsk_gpu__staged_stats) */
+    uint8_t* h_stage;   /* STAGED without an alias: pinned host staging, two halves of STAGE_HALF (allocated on first use) */
+    uint8_t* d_stage;   /* its device copy */
+    hipEvent_t stage_ev[2]; /* the DMA copy that last read each host half ... */
+    int stage_rec[2];       /* ... once one has */
+    int stage_half;     /* the half the next host pack fills */
+    uint64_t stage_bytes; /* bytes per half (STAGE_HALF; xsk_gpu__staged_noalias sets others for tests) */
     int registered;   /* this context registered the UMEM (and unregisters it at fini) */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
@@ -165,6 +171,10 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
     (void)hipFree(c->d_stats);
     for (int s = 0; s < NSTREAMS; s++) (void)hipFree(c->d_ws[s]);
     (void)hipFree(c->d_pack);
+    (void)hipFree(c->d_stage);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    for (int h = 0; h < 2; h++)
+        if (c->stage_ev[h]) (void)hipEventDestroy(c->stage_ev[h]);
     if (c->h_pack) (void)hipHostFree(c->h_pack);
     if (c->h_verd) (void)hipHostFree(c->h_verd);
     if (c->h_stats) (void)hipHostFree(c->h_stats);
@@ -211,6 +221,7 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     c->umem_size = umem_size;
     c->max_batch = max_batch;
     c->max_chunks = mode == XSK_GPU_MODE_STAGED ? stage_chunks_max(max_batch) : 1;
+    c->stage_bytes = STAGE_HALF;
     TRY(hipSetDevice(device));
     for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamCreateWithFlags(&c->stream[s], hipStreamNonBlocking));
     if (!prereg) { /* mapped in every mode: STAGED's gather kernel reads scattered frames through the alias */
@@ -300,24 +311,21 @@ void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* c) {
     xsk_gpu__lowlat_stop(c->ll);
 }
 
-int xsk_gpu__staged_stats(const xsk_gpu_ctx* c, uint64_t out[5]) {
+int xsk_gpu__staged_stats(const xsk_gpu_ctx* c, uint64_t out[XSK_GPU__STAGED_STATS]) {
     if (!c || !out || c->mode != XSK_GPU_MODE_STAGED) return -EINVAL;
-    for (int i = 0; i < 5; i++) out[i] = c->staged[i];
+    for (int i = 0; i < XSK_GPU__STAGED_STATS; i++) out[i] = c->staged[i];
+    return 0;
+}
+int xsk_gpu__staged_noalias(xsk_gpu_ctx* c, uint32_t half_bytes) {
+    if (!c || c->mode != XSK_GPU_MODE_STAGED || (half_bytes && (half_bytes < 4096u || (half_bytes & 15u))) ||
+        c->h_stage)
+        return -EINVAL;
+    c->m_umem = NULL;
+    if (half_bytes) c->stage_bytes = half_bytes;
     return 0;
 }
 int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
 xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
-
-/* Uniform stride S (>= 64, multiple of 16) when addr[i] = addr[0] + i*S for the whole chunk. */
-static uint64_t uniform_stride(const struct xsk_gpu_desc* d, uint32_t n) {
-    if (n < 2) return 0;
-    if (d[1].addr <= d[0].addr) return 0;
-    const uint64_t s = d[1].addr - d[0].addr;
-    if (s < 64 || (s & 15u)) return 0;
-    for (uint32_t i = 2; i < n; i++)
-        if (d[i].addr != d[0].addr + (uint64_t)i * s) return 0;
-    return s;
-}
 
 int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     if (!c || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
@@ -330,79 +338,104 @@ int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     return 0;
 }
 
-/* Copy-in of the bytes the transform reads for frames d[0..n) (xsk_gpu__read_span) into the device mirror:
- *   - n <= XSK_GPU_LOWLAT_MAX (an RX-loop batch): the gather kernel below, whatever the layout;
- *   - a uniform frame stride whose strided rows carry at most 10 % more than those bytes: one 2-D DMA copy;
- *   - frames covering their span [lo, hi) densely (at most 10 % of it between frames): one DMA copy of the span;
- *   - otherwise -- AF_XDP's recycled descriptors scatter over the UMEM (xsk_receive.c:55-71, :201-217, :226-227) --
- *     the gather kernel moves each frame's own bytes across PCIe (dd: the chunk's descriptors, already on the device).
- * So a call never copies more than 1.1 x the bytes its frames own (c->staged[0] counts them).  stage_plan decides,
- * stage_issue enqueues.  `contained`: the copy writes no mirror byte outside the chunk's own frames -- every frame
- * 16-B aligned (a frame's read span then ends at or before the next 16-B aligned frame: include/xsk_gpu.h's
- * ownership contract) and not the span copy; only then may it run beside another chunk's transform. */
-enum { STAGE_NONE, STAGE_2D, STAGE_SPAN, STAGE_GATHER };
-struct stage_plan {
-    int kind;
-    int contained;
-    uint64_t lo, hi, base, stride, width, sum;
-};
-static struct stage_plan stage_plan(const xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n) {
+/* STAGED without a mapped alias, scattered frames (XSK_STAGE_HOSTPACK): the host copies the chunk's read spans back
+ * to back into a half of the pinned staging -- a table of u32 offsets first, then the spans, each at a 16-B aligned
+ * offset -- one DMA copy moves the half, and the unpack kernel puts every span at its offset in the mirror.  A half is
+ * refilled once the DMA copy that last read it has finished (its event), so the host packs half h while half h ^ 1 is
+ * in flight.  A frame whose span cannot fit a half moves by a DMA copy of its own.  The bytes moved are the spans plus
+ * 4 per frame of offsets: never the gaps between frames. */
+static int stage_hostpack(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const struct xsk_gpu_desc* dd, uint32_t n,
+                          hipStream_t st) {
     const int wire = c->opts != 0;
-    struct stage_plan p = {STAGE_NONE, 1, UINT64_MAX, 0, 0, 0, 0, 0};
-    uint64_t unaligned = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        unaligned |= d[i].addr & 15u;
-        uint64_t a16 = 0;
-        const uint64_t sp = xsk_gpu__read_span(d[i].addr, d[i].len, c->umem_size, wire, &a16);
-        if (!sp) continue; /* the transform reads nothing of this frame */
-        if (a16 < p.lo) p.lo = a16;
-        if (a16 + sp > p.hi) p.hi = a16 + sp;
-        if (sp > p.width) p.width = sp;
-        p.sum += sp;
+    const uint64_t half = c->stage_bytes;
+    if (!c->h_stage) { /* first use */
+        if (hipHostMalloc((void**)&c->h_stage, 2u * (size_t)half, hipHostMallocDefault) != hipSuccess) {
+            c->h_stage = NULL;
+            return -ENOMEM;
+        }
+        if (hipMalloc((void**)&c->d_stage, 2u * (size_t)half) != hipSuccess) {
+            c->d_stage = NULL;
+            return -ENOMEM;
+        }
+        for (int h = 0; h < 2; h++)
+            if (hipEventCreateWithFlags(&c->stage_ev[h], hipEventDisableTiming) != hipSuccess) return -EIO;
     }
-    if (!p.sum) return p;
-    const uint64_t budget = p.sum + p.sum / 10;
-    p.stride = uniform_stride(d, n);
-    p.base = d[0].addr & ~15ull;
-    p.contained = unaligned == 0;
-    /* an RX-loop-sized batch takes the gather kernel whatever its layout: one launch beats a DMA submission there
-     * (64 x 64 B: 55.7 us per call vs 66.1 with the 2-D copy; 1024 x 1500 B: 126.2 vs 129.0 --
-     * profiles/r04/pass1/hostlat_*.jsonl) */
-    const int small = n <= XSK_GPU_LOWLAT_MAX && c->m_umem;
-    const uint64_t s = p.stride;
-    if (!small && s && p.width <= s && (uint64_t)n * p.width <= budget &&
-        p.base + (uint64_t)(n - 1) * s + p.width <= c->umem_size)
-        p.kind = STAGE_2D;
-    else if (!small && (p.hi - p.lo <= budget || !c->m_umem)) { /* (no mapped alias: the span, ordered) */
-        p.kind = STAGE_SPAN;
-        p.contained = 0;
-    } else
-        p.kind = STAGE_GATHER;
-    return p;
+    for (uint32_t f0 = 0; f0 < n;) {
+        /* the frames [f0, f1) whose offsets table and spans fit one half (a frame too large for any half: 0 bytes) */
+        uint32_t f1 = f0;
+        uint64_t bytes = 0;
+        for (; f1 < n; f1++) {
+            uint64_t a16 = 0;
+            const uint64_t sp = xsk_gpu__read_span(d[f1].addr, d[f1].len, c->umem_size, wire, &a16);
+            const uint64_t b = sp + 16u > half ? 0u : sp;
+            if ((((uint64_t)(f1 - f0 + 1) * 4u + 15u) & ~15ull) + bytes + b > half) break;
+            bytes += b;
+        }
+        const int h = c->stage_half;
+        if (c->stage_rec[h] && hipEventSynchronize(c->stage_ev[h]) != hipSuccess) return -EIO;
+        uint8_t* hs = c->h_stage + (size_t)h * half;
+        uint8_t* ds = c->d_stage + (size_t)h * half;
+        uint32_t* offs = (uint32_t*)hs;
+        const uint32_t m = f1 - f0;
+        const uint64_t data0 = ((uint64_t)m * 4u + 15u) & ~15ull;
+        uint64_t pos = data0;
+        for (uint32_t f = f0; f < f1; f++) {
+            uint64_t a16 = 0;
+            const uint64_t sp = xsk_gpu__read_span(d[f].addr, d[f].len, c->umem_size, wire, &a16);
+            if (sp + 16u > half) { /* too large for any half: its own DMA copy */
+                if (hipMemcpyAsync(c->d_umem + a16, c->umem + a16, sp, hipMemcpyHostToDevice, st) != hipSuccess)
+                    return -EIO;
+                c->staged[0] += sp;
+                c->staged[6]++;
+                offs[f - f0] = UINT32_MAX;
+                continue;
+            }
+            offs[f - f0] = (uint32_t)(pos - data0);
+            memcpy(hs + pos, c->umem + a16, sp);
+            pos += sp;
+        }
+        if (hipMemcpyAsync(ds, hs, pos, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipEventRecord(c->stage_ev[h], st) != hipSuccess)
+            return -EIO;
+        c->stage_rec[h] = 1;
+        const int rc = xsk_gpu__stage_unpack_dev(ds + data0, (const uint32_t*)ds, c->d_umem, c->umem_size, dd + f0, m,
+                                                 (uint32_t)wire, st);
+        if (rc) return rc;
+        c->staged[0] += pos; /* the offsets table (padded to 16 B) and the spans */
+        c->stage_half ^= 1;
+        f0 = f1;
+    }
+    c->staged[5]++;
+    return 0;
 }
-static int stage_issue(xsk_gpu_ctx* c, const struct stage_plan* p, const struct xsk_gpu_desc* dd, uint32_t n,
-                       hipStream_t st) {
+
+/* Enqueue the copy-in chunk d[0..n) planned as p (dd: the chunk's descriptors, already on the device) on stream st;
+ * c->staged records the bytes (never more than 1.1 x the frames' read spans, plus the host pack's offsets). */
+static int stage_issue(xsk_gpu_ctx* c, const struct xsk_stage_plan* p, const struct xsk_gpu_desc* d,
+                       const struct xsk_gpu_desc* dd, uint32_t n, hipStream_t st) {
     switch (p->kind) {
-        case STAGE_2D:
+        case XSK_STAGE_2D:
             if (hipMemcpy2DAsync(c->d_umem + p->base, p->stride, c->umem + p->base, p->stride, p->width, n,
                                  hipMemcpyHostToDevice, st) != hipSuccess)
                 return -EIO;
             c->staged[0] += (uint64_t)n * p->width;
             c->staged[1]++;
             return 0;
-        case STAGE_SPAN:
+        case XSK_STAGE_SPAN:
             if (hipMemcpyAsync(c->d_umem + p->lo, c->umem + p->lo, p->hi - p->lo, hipMemcpyHostToDevice, st) != hipSuccess)
                 return -EIO;
             c->staged[0] += p->hi - p->lo;
             c->staged[2]++;
             return 0;
-        case STAGE_GATHER: {
+        case XSK_STAGE_GATHER: {
             const int rc = xsk_gpu__stage_gather_dev(c->m_umem, c->d_umem, c->umem_size, dd, n, (uint32_t)(c->opts != 0), st);
             if (rc) return rc;
             c->staged[0] += p->sum;
             c->staged[3]++;
             return 0;
         }
+        case XSK_STAGE_HOSTPACK:
+            return stage_hostpack(c, d, dd, n, st);
         default:
             return 0;
     }
@@ -411,7 +444,7 @@ static int stage_issue(xsk_gpu_ctx* c, const struct stage_plan* p, const struct 
 /* Enqueue one chunk [i0, i0+n) of the batch (ZEROCOPY: on stream s); results land in the pinned host buffers
  * and c->done[ci] fires when they are there. */
 static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t i0, uint32_t n, uint32_t ci,
-                         int want_recs, int s) {
+                         int want_recs, int s, int* prefix_aligned) {
     int rc = 0;
     if (zerocopy(c)) { /* descriptors in, verdicts and counters out: mapped host memory */
         const hipStream_t st = c->stream[s];
@@ -427,18 +460,21 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
     /* STAGED: the copy stream (stream[0]) takes every chunk's descriptors and copy-in back to back, so the H2D
      * direction of the link never waits for a transform; the compute stream (stream[1]) runs each chunk's
      * transform once its copy-in is in, then its header pack and the copy-back.  A copy-in that may write mirror
-     * bytes of other chunks' frames (not contained: an unaligned frame's span reaches into its neighbour, the span
-     * copy covers whatever lies between) first waits for the previous chunk's pack, and so for every earlier
-     * chunk's (the compute stream is in order); later chunks' transforms follow their own copy-ins, which follow
-     * this one on the copy stream.  Contained copy-ins run under the other chunks' transforms. */
+     * bytes of an earlier chunk's frames (not contained, xsk_stage_plan.h: an unaligned frame anywhere in the call so
+     * far, a span or a 2-D row reaching past the frame's own bytes, the dense-span copy) first waits for the previous
+     * chunk's pack, and so for every earlier chunk's (the compute stream is in order); later chunks' transforms
+     * follow their own copy-ins, which follow this one on the copy stream.  Contained copy-ins run under the other
+     * chunks' transforms. */
     (void)s;
     const hipStream_t sa = c->stream[0], sb = c->stream[1];
     struct xsk_gpu_desc* dd = c->d_descs + i0;
     TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, sa));
-    const struct stage_plan p = stage_plan(c, descs + i0, n);
+    const struct xsk_stage_plan p =
+        xsk_gpu__stage_plan(descs + i0, n, c->umem_size, c->opts != 0, c->m_umem != NULL, *prefix_aligned);
+    *prefix_aligned &= (int)p.aligned;
     if (ci > 0 && !p.contained) TRY(hipStreamWaitEvent(sa, c->packed[ci - 1], 0));
     if (p.contained) c->staged[4]++;
-    rc = stage_issue(c, &p, dd, n, sa);
+    rc = stage_issue(c, &p, descs + i0, dd, n, sa);
     if (rc) goto out;
     TRY(hipEventRecord(c->in_done[ci], sa));
     TRY(hipStreamWaitEvent(sb, c->in_done[ci], 0));
@@ -513,13 +549,16 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
         }
         return 0;
     }
+    int caller_dev = -1; /* the caller's current device, restored on return */
+    if (hipGetDevice(&caller_dev) != hipSuccess) caller_dev = -1;
     TRY(hipSetDevice(c->device));
     if (c->ll) xsk_gpu__lowlat_stop(c->ll); /* a large batch: the launch path (its streams never wait on it) */
     const int staged = c->mode == XSK_GPU_MODE_STAGED;
     uint32_t nchunks = 0;
+    int prefix_aligned = 1; /* every frame of the chunks enqueued so far starts 16-B aligned */
     for (uint32_t i0 = 0; i0 < n; nchunks++) {
         const uint32_t m = staged ? stage_chunk(n, n - i0) : n;
-        rc = enqueue_chunk(c, descs, i0, m, nchunks, recs != NULL, (int)(nchunks % NSTREAMS));
+        rc = enqueue_chunk(c, descs, i0, m, nchunks, recs != NULL, (int)(nchunks % NSTREAMS), &prefix_aligned);
         if (rc) goto drain;
         i0 += m;
     }
@@ -550,9 +589,10 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
         for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamSynchronize(c->stream[s]));
         TRY(hipMemcpy(recs, c->d_recs, (size_t)n * sizeof *recs, hipMemcpyDeviceToHost));
     }
-    return 0;
+    goto out;
 drain:
     for (int s = 0; s < NSTREAMS; s++) (void)hipStreamSynchronize(c->stream[s]);
 out:
+    if (caller_dev >= 0 && caller_dev != c->device) (void)hipSetDevice(caller_dev);
     return rc;
 }

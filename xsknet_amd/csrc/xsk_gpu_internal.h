@@ -21,8 +21,9 @@ XSK_GPU__HIDDEN int xsk_gpu__pack_headers_dev(const void* d_umem, const struct x
 
 /* The bytes the transform reads of one frame, [*a16, *a16 + return value): for a frame it parses (reference mode:
  * len >= 20, wire mode: len >= 14, the descriptor inside the UMEM) its 16-B aligned start up to
- * align16(max(off + len, its header window inside the UMEM)); 0 for a frame it reads nothing of (xsk_echo_device.h,
- * echo6_body step 1).  Host and device (staged mode's copy-in, xsk_gpu_host.c, and its gather kernel). */
+ * align16(max(off + len, its 64-B header window inside the UMEM)) -- both modes read the same window since round 4
+ * (xsk_echo_device.h, frame_in / echo6_body step 1: lim = max(rowhi, wend)); 0 for a frame it reads nothing of.
+ * Host and device (staged mode's copy-in, xsk_gpu_host.c, and its gather kernel). */
 #ifdef __HIPCC__
 __host__ __device__
 #endif
@@ -31,7 +32,7 @@ static inline uint64_t xsk_gpu__read_span(uint64_t addr, uint32_t len, uint64_t 
     const uint64_t need = wire ? len : (len >= 20u ? (len > 38u ? len : 38u) : len);
     if (len > XSK_GPU_MAX_LEN || addr > umem_size || need > umem_size - addr || len < (wire ? 14u : 20u)) return 0;
     const uint64_t off = addr & 15u;
-    const uint64_t win = wire ? 128u : 64u;
+    const uint64_t win = 64u;
     const uint64_t wend = umem_size - *a16 < win ? umem_size - *a16 : win;
     const uint64_t lim = off + len > wend ? off + len : wend;
     return (lim + 15u) & ~15ull;
@@ -44,6 +45,12 @@ static inline uint64_t xsk_gpu__read_span(uint64_t addr, uint32_t len, uint64_t 
 XSK_GPU__HIDDEN int xsk_gpu__stage_gather_dev(const void* m_umem, void* d_mirror, uint64_t umem_size,
                                               const struct xsk_gpu_desc* d_descs, uint32_t n, uint32_t wire,
                                               void* stream);
+/* xsk_aux.hip: the same per-frame copy from a device staging buffer the host packed the read spans into (a context
+ * whose device has no mapped alias of the UMEM): frame f's span is at d_stage + d_offs[f] (16-B aligned), or nowhere
+ * when d_offs[f] == UINT32_MAX (the host copied that frame itself). */
+XSK_GPU__HIDDEN int xsk_gpu__stage_unpack_dev(const void* d_stage, const uint32_t* d_offs, void* d_mirror,
+                                              uint64_t umem_size, const struct xsk_gpu_desc* d_descs, uint32_t n,
+                                              uint32_t wire, void* stream);
 
 /* xsk_echo.hip: xsk_gpu_echo_dev_opts for counters in mapped host memory (no device atomics): d_stats
  * must be a slot zeroed for this call (a one-workgroup launch stores the counters without reading it).
@@ -119,11 +126,21 @@ XSK_GPU__HIDDEN uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* ctx);
 /* xsk_gpu_host.c: stop the context's resident LOWLAT kernel, if any, and wait for it (the multi-context path stops
  * every context's before a batch whose shares take the launch path). */
 XSK_GPU__HIDDEN void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* ctx);
-/* xsk_gpu_host.c (exported for the GPU tests, not part of the ABI): a STAGED context's copy-in record since init --
- * out[0] bytes copied host->device, out[1..3] chunks copied as one 2-D stride / one dense span / by the gather
- * kernel, out[4] chunks whose copy-in was contained (not ordered after the previous chunk's pack).  -EINVAL for other
- * modes. */
-int xsk_gpu__staged_stats(const xsk_gpu_ctx* ctx, uint64_t out[5]);
+/* xsk_gpu_host.c (exported for the GPU tests and the bench, not part of the ABI): a STAGED context's copy-in record
+ * since init -- out[0] bytes copied host->device (frame bytes, plus the staging offsets of the host pack), out[1..3]
+ * chunks copied as one 2-D stride / one dense span / by the gather kernel, out[4] chunks whose copy-in was contained
+ * (not ordered after the previous chunk's pack), out[5] chunks copied by the host pack (no mapped alias on the
+ * context's device), out[6] frames of those copied by a DMA copy of their own (a span larger than a staging half).
+ * -EINVAL for other modes. */
+#define XSK_GPU__STAGED_STATS 7
+int xsk_gpu__staged_stats(const xsk_gpu_ctx* ctx, uint64_t out[XSK_GPU__STAGED_STATS]);
+/* xsk_gpu_host.c (test switch, not part of the ABI): a STAGED context forgets its UMEM's mapped device alias, as on a
+ * device where the runtime gives none, so its scattered copy-ins take the host pack, with staging halves of half_bytes
+ * (0 = the default 32 MiB; else >= 4096 and a multiple of 16, so that tests reach the frames too large for a half).
+ * -EINVAL for other modes, bad sizes, or once the host pack has run. */
+int xsk_gpu__staged_noalias(xsk_gpu_ctx* ctx, uint32_t half_bytes);
+/* xsk_gpu_multi.c (tests and the bench, not part of the ABI): context g of a multi object, or NULL. */
+xsk_gpu_ctx* xsk_gpu__multi_ctx(xsk_gpu_multi* m, uint32_t g);
 
 /* xsk_lowlat.hip: the low-latency doorbell channel of a XSK_GPU_MODE_LOWLAT context (doorbell layout and
  * host protocol: xsk_lowlat_proto.h). */

@@ -207,8 +207,14 @@ int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, ui
      * share fits it; otherwise every context takes the launch path, and every resident kernel has stopped before
      * any share is launched, so no share runs beside a resident kernel that holds a CU */
     m->job_launch = !m->all_lowlat || (n + m->G - 1) / m->G > XSK_GPU_LOWLAT_MAX;
-    if (m->job_launch)
+    /* (with a downgraded context no batch ever takes a doorbell, so no resident kernel is ever started: nothing to
+     * stop, per call or otherwise -- ADVICE r04) */
+    if (m->job_launch && m->all_lowlat) {
+        int dev = -1;
+        const int have = hipGetDevice(&dev) == hipSuccess;
         for (uint32_t g = 0; g < m->G; g++) xsk_gpu__ctx_quiesce(m->w[g].ctx);
+        if (have) (void)hipSetDevice(dev); /* the caller's current device, as it was */
+    }
     if (m->G > 1) {
         pthread_mutex_lock(&m->mu);
         m->pending = m->G - 1;
@@ -235,6 +241,8 @@ int xsk_gpu_multi_status(const xsk_gpu_multi* m, int* status, uint32_t cap) {
     for (uint32_t g = 0; g < m->G && g < cap; g++) status[g] = m->status[g];
     return (int)m->G;
 }
+
+xsk_gpu_ctx* xsk_gpu__multi_ctx(xsk_gpu_multi* m, uint32_t g) { return m && g < m->G ? m->w[g].ctx : NULL; }
 
 int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc) {
     if (!m || g >= m->G || rc >= 0) return -EINVAL;

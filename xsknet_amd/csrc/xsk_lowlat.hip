@@ -206,7 +206,7 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
 // descriptor slots with the doorbell and owns `alive` and the idle exit.
 template <bool WIRE>
 __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
-    __shared__ Echo6Smem<kLLTPW, false> sm;  // 64-B windows in both modes (wire: wire_header_phase64)
+    __shared__ Echo6Smem<kLLTPW> sm;  // 64-B windows in both modes (wire: wire_header_phase64)
     __shared__ uint32_t s_cmd[4];  // work?, n, recs | tile | dl, f0
     // the body's phase stamps land in the LDS and go to the device-memory diagnostics after `done`: a store
     // to host memory would put its PCIe acknowledgement in front of every later wait on a load (the
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         if (ntiles)
             // wire mode on the reference form's 64-B windows and streams with wire_header_phase64 (the 128-B form took
             // 11.6 us per 64 x 64-B call with every option against 8.7 in reference mode, profiles/r04/wll/)
-            echo6_body<kLLTPW, kLLSync, WIRE, true, true, true, false, kRefHeavy, kU, false, false, 0, 1, 0, kWin>(a, 0u,
+            echo6_body<kLLTPW, kLLSync, WIRE, true, true, true, false, kRefHeavy, kU, false, false, 0>(a, 0u,
                                                                                                           ntiles, sm);
         // the two polls' registers live across the body: a batch is taken while the other poll is still in
         // flight, and registers the compiler reused would first have to wait for it to land
