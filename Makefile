@@ -1,7 +1,7 @@
 # Build of the MI355X (gfx950) echo-transform library and its C tools.
 #   make            -> xsknet_amd/libxsknet_amd.so (the product), xsknet_amd/libxsknet_amd_tune.so (the product kernel
 #                      at alternative switch values, for tools/abbench.py and its parity tests only), oracle/liboracle.so,
-#                      tools/echo_replay, tools/rxqueues
+#                      tools/echo_replay, tools/rxqueues, tools/rxring
 ROCM     ?= /opt/rocm
 HIPCC    ?= $(ROCM)/bin/hipcc
 CC       := gcc
@@ -12,7 +12,7 @@ CSRC     := xsknet_amd/csrc
 LIB      := xsknet_amd/libxsknet_amd.so
 TUNELIB  := xsknet_amd/libxsknet_amd_tune.so
 
-all: $(LIB) $(TUNELIB) oracle tools/echo_replay tools/rxqueues
+all: $(LIB) $(TUNELIB) oracle tools/echo_replay tools/rxqueues tools/rxring
 
 # every header a device object or a host object may include (the doorbell layout and host protocol of
 # xsk_lowlat_proto.h are shared by xsk_lowlat.hip and xsk_gpu_host.c)
@@ -51,11 +51,14 @@ tools/echo_replay: tools/echo_replay.c $(LIB) include/xsk_gpu.h
 tools/rxqueues: tools/rxqueues.c $(LIB) include/xsk_gpu.h
 	$(CC) $(CFLAGS) -o $@ $< -L xsknet_amd -lxsknet_amd -pthread -Wl,-rpath,'$$ORIGIN/../xsknet_amd'
 
+tools/rxring: tools/rxring.c $(LIB) include/xsk_gpu.h
+	$(CC) $(CFLAGS) -o $@ $< -L xsknet_amd -lxsknet_amd -pthread -Wl,-rpath,'$$ORIGIN/../xsknet_amd'
+
 oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay tools/rxqueues
+	rm -f $(CSRC)/*.o $(CSRC)/tune/*.o $(LIB) $(TUNELIB) tools/echo_replay tools/rxqueues tools/rxring
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

@@ -55,7 +55,9 @@ def uniform_stride(addrs):
 
 
 def stage_plan(descs, umem_size, wire=False, have_alias=True, prefix_aligned=True):
-    """Returns (kind, contained, aligned, sum): which path copies chunk `descs` into the device mirror, and whether the
+    """Returns (kind, contained, aligned, sum, moved): which path copies chunk `descs` into the device mirror (sum: the
+    frames' read spans; moved: the frame bytes that path copies -- n x width for the 2-D copy, the span for the span
+    copy, the spans otherwise; the host pack adds its offset tables), and whether the
     copy writes only mirror bytes of the chunk's own frames -- [addr, align16(addr + max(len, 64))) of each -- while
     every frame of the call so far (earlier chunks included) starts 16-B aligned, so that no earlier chunk's frame can
     be overwritten while its transform and header pack are in flight."""
@@ -76,16 +78,16 @@ def stage_plan(descs, umem_size, wire=False, have_alias=True, prefix_aligned=Tru
         width = max(width, sp)
         total += sp
     if not total:
-        return NONE, True, aligned, 0
+        return NONE, True, aligned, 0, 0
     budget = total + total // 10
     s = uniform_stride(addrs)
     base = addrs[0] & ~15
     small = n <= LOWLAT_MAX and have_alias
     if not small and s and width <= s and n * width <= budget and base + (n - 1) * s + width <= umem_size:
-        return TWO_D, prefix and width <= min_own, aligned, total
+        return TWO_D, prefix and width <= min_own, aligned, total, n * width
     if not small and hi - lo <= budget:
-        return SPAN, False, aligned, total
-    return (GATHER if have_alias else HOSTPACK), prefix and spans_own, aligned, total
+        return SPAN, False, aligned, total, hi - lo
+    return (GATHER if have_alias else HOSTPACK), prefix and spans_own, aligned, total, total
 
 
 def call_plans(descs, umem_size, wire=False, have_alias=True):

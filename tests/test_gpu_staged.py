@@ -78,22 +78,30 @@ def test_staged_scrambled_multi_chunk():
 def test_staged_strided_multi_chunk_back_to_back():
     """The host-inclusive bench's shape (1500-B frames at a 4 KiB stride, 16-B aligned) over 3 x 32 768 + 777 frames:
     every chunk's 2-D copy-in is contained, so the copy-ins run back to back on the copy stream under the other
-    chunks' transforms and packs -- exact, three times."""
+    chunks' transforms and packs -- exact, three times.  Then the same layout with the generator's mixed traffic (a
+    tenth of the frames 0-42 B long, negatives): a short frame's 1504-B row runs past the 64 bytes it owns, so those
+    chunks' 2-D copies are ordered after the previous pack (round 4 ran them contained) -- exact too."""
     _dev()
     n = 3 * CHUNK + 777
-    umem = np.zeros(n * 4096, np.uint8)
-    descs = oracle.synth_batch(umem, n, 0, 4096, 0x5EED4C05, mode=1, len_lo=1500, len_hi=1500,
-                               threads=min(16, oracle.cpu_threads()))
-    for rep in range(3):
-        work = umem.copy()
-        with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
-            v, r, st = ctx.process(descs)
-            rec = ctx.staged_stats()
-        check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
-        # (a tail chunk of <= 1024 frames is RX-loop sized: the gather kernel)
+    for mode in (0, 1):
+        umem = np.zeros(n * 4096, np.uint8)
+        descs = oracle.synth_batch(umem, n, 0, 4096, 0x5EED4C05, mode=mode, len_lo=1500, len_hi=1500,
+                                   threads=min(16, oracle.cpu_threads()))
+        plans = SP.call_plans(descs, umem.nbytes)
         ch = stage_chunks(n)
-        small = sum(m <= 1024 for m in ch)
-        assert rec["contained"] == len(ch) and rec["strided"] == len(ch) - small and rec["gather"] == small, (rec, ch)
+        small = sum(m <= 1024 for m in ch)  # (a tail chunk of <= 1024 frames is RX-loop sized: the gather kernel)
+        if mode == 0:
+            assert all(p[1] for p in plans)
+        else:
+            assert not any(p[1] for p in plans if p[0] == SP.TWO_D)
+        for rep in range(3 if mode == 0 else 1):
+            work = umem.copy()
+            with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
+                v, r, st = ctx.process(descs)
+                rec = ctx.staged_stats()
+            check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
+            assert rec["contained"] == sum(p[1] for p in plans) and rec["strided"] == len(ch) - small and \
+                rec["gather"] == small, (rec, ch, plans)
 
 
 def packed(lens, seed):
@@ -300,7 +308,7 @@ def test_staged_wire_64b_pitch_interleaved():
         assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all(), rep
         for k in COUNTERS:
             assert int(st[k]) == int(s_ref[k]), k
-        assert rec["contained"] == sum(p[1] for p in plans) and rec["h2d_bytes"] == sum(p[3] for p in plans), (rec, plans)
+        assert rec["contained"] == sum(p[1] for p in plans) and rec["h2d_bytes"] == sum(p[4] for p in plans), (rec, plans)
 
 
 # ---- STAGED without a mapped alias: the host pack ---------------------------------------------
@@ -410,6 +418,43 @@ def test_lowlat_timeout_exactly_once():
                 v, r, _ = ctx.process(descs)  # the retry
                 assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
     print("timeout outcomes:", outcomes)
+
+
+def test_lowlat_partial_timeout_deterministic():
+    """the partly-served timeout path, made to happen.  A hog kernel holds every CU for 300 ms except one on
+    each even XCC (released after 1 ms), then a LOWLAT call posts 1024 x 1500-B frames to a fresh resident grid of four
+    workgroups with a 20-ms timeout: the grid's workgroups go round-robin over four consecutive XCCs, so two of them find
+    a CU and serve their slices and two wait behind the hog.  At the timeout the call posts STOP and waits for the grid; when the hog ends, 2 and 3 start, find STOP and
+    retire their slices unserved -- so the call finishes those two slices through the launch path and returns 0.  The
+    output must be exactly the oracle's, and the context must count the batch as a partial completion."""
+    _dev()
+    n = 1024
+    umem = np.zeros(n * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED6161, mode=0, len_lo=1500, len_hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    hog = torch.cuda.Stream()
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_LOWLAT) as ctx:
+        assert ctx.mode == X.MODE_LOWLAT
+        ctx.lowlat_tune(groups=4, timeout_us=20000)
+        claim = torch.zeros(8, dtype=torch.int32, device="cuda:0")
+        torch.cuda.synchronize()
+        assert X.tune_lib().xsk_gpu__test_hog(ncu, 300000, 0x55, claim.data_ptr(), hog.cuda_stream) == 0
+        time.sleep(0.01)  # the hog's workgroups are resident, the early ones gone
+        v, r, st = ctx.process(descs)
+        out = ctx.lowlat_outcomes()
+        hog.synchronize()
+        print("hog claims per XCC:", claim.tolist(), "outcomes:", out)
+        assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
+        assert int(st["tx_packets"]) == int(s_ref["tx_packets"]) and int(st["rx_bytes"]) == int(s_ref["rx_bytes"])
+        assert out == {"timeouts": 1, "partial": 1, "untouched": 0}, out
+        # the context works on afterwards (its grid relaunched by the next batch)
+        ctx.lowlat_tune(groups=0, timeout_us=0)
+        work[:] = umem
+        v, r, _ = ctx.process(descs)
+        assert (v == v_ref).all() and (work == ref).all()
 
 
 def test_lowlat_reserved_queue_for_an_application_stream():

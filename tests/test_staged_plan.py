@@ -65,7 +65,9 @@ def cplan():
         d = np.ascontiguousarray(d, DESC)
         out = (C.c_uint64 * 9)()
         L.xsk_test_stage_plan(d.ctypes.data, len(d), umem_size, int(wire), int(have_alias), int(prefix), out)
-        return int(out[0]), bool(out[1]), bool(out[2]), int(out[8])
+        kind, n = int(out[0]), len(d)
+        moved = {SP.TWO_D: n * int(out[7]), SP.SPAN: int(out[4]) - int(out[3])}.get(kind, int(out[8]))
+        return kind, bool(out[1]), bool(out[2]), int(out[8]), (moved if int(out[8]) else 0)
     return plan
 
 
@@ -180,7 +182,7 @@ def test_plan_no_alias_bounded():
     for n in (64, 1024, SP.CHUNK_FRAMES):
         addrs = 256 + rng.permutation(4 * n)[:n].astype(np.int64) * 4096
         d = _descs(addrs, rng.integers(20, 1500, n))
-        kind, contained, aligned, total = SP.stage_plan(d, 16 * n * 4096, have_alias=False)
+        kind, contained, aligned, total, _ = SP.stage_plan(d, 16 * n * 4096, have_alias=False)
         assert kind == SP.HOSTPACK and contained and aligned
         owned = int((((np.maximum(d["len"].astype(np.int64), 64) + 15) // 16) * 16).sum())
         assert total + 4 * n <= 1.1 * owned

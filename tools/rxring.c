@@ -1,0 +1,281 @@
+/*
+ * rxring.c — RX-loop throughput per queue under a saturated RX ring: xsk_gpu_rx_step() against
+ * a simulated kernel side of the AF_XDP rings, the loop of the reference's client (src/lib/xsk_receive.c:192-237 with
+ * complete_tx() :77-99) with the transform on the GPU.
+ *
+ * Per queue (one thread, one UMEM, one context, its four rings):
+ *   - the simulated NIC (untimed): takes every TX descriptor, checks the frame is the exact echo reply of the request
+ *     it delivered there (every byte of the frame), and posts its address on the completion ring; then receives a
+ *     request into every frame the fill ring hands it (the chunk base + the 256-B XDP headroom, as the kernel does in
+ *     aligned-chunk mode) until the RX ring is full -- the ring stays saturated;
+ *   - the application loop (timed): xsk_gpu_tx_complete() (complete_tx minus the kick) and one xsk_gpu_rx_step() of up
+ *     to <step> descriptors.
+ * A step takes min(ring occupancy, step, XSK_GPU_RX_MAX_STEP) frames; the reference's RX_BATCH_SIZE (64,
+ * src/lib/xsk_utils.h:8) is a constant of its CPU loop and changes no frame's result.
+ *
+ *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0]
+ *
+ * empty=1: the empty-ring latency instead -- the NIC delivers exactly <step> frames, the step serves them, repeat
+ * (each call finds exactly its batch: the RX-loop latency of tools/hostlat.py, through the ring loop).
+ * Prints one JSON line: Mframes/s per queue and in total (frames / the timed application time), us per step (mean,
+ * p50, p99), frames checked, failures.  Tool only: it builds its own frames and links only libxsknet_amd.
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "../include/xsk_gpu.h"
+
+#define CHUNK 4096u
+#define HEADROOM 256u
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static uint16_t csum16(const uint8_t* p, size_t n) { /* RFC 1071 over network-order bytes */
+    uint32_t s = 0;
+    for (size_t i = 0; i + 1 < n; i += 2) s += (uint32_t)p[i] << 8 | p[i + 1];
+    if (n & 1) s += (uint32_t)p[n - 1] << 8;
+    while (s >> 16) s = (s & 0xFFFFu) + (s >> 16);
+    return (uint16_t)~s;
+}
+
+/* An ICMP echo request of `len` (>= 42) bytes, valid checksums, and its reply as the reference writes it
+ * (xsk_receive.c:148-157: MACs and IPv4 addresses swapped, type 0, checksum by csum_replace2). */
+static void make_pair(uint8_t* req, uint8_t* rep, uint32_t len, uint32_t q) {
+    memset(req, 0, len);
+    const uint8_t dst[6] = {0x02, 0, 0, 0, (uint8_t)q, 1}, src[6] = {0x02, 0, 0, 0, (uint8_t)q, 2};
+    memcpy(req, dst, 6);
+    memcpy(req + 6, src, 6);
+    req[12] = 0x08;
+    uint8_t* ip = req + 14;
+    ip[0] = 0x45;
+    ip[2] = (uint8_t)((len - 14) >> 8);
+    ip[3] = (uint8_t)(len - 14);
+    ip[8] = 64;
+    ip[9] = 1;
+    ip[12] = 10, ip[14] = (uint8_t)q, ip[15] = 2;
+    ip[16] = 10, ip[18] = (uint8_t)q, ip[19] = 1;
+    const uint16_t ic = csum16(ip, 20);
+    ip[10] = (uint8_t)(ic >> 8), ip[11] = (uint8_t)ic;
+    uint8_t* icmp = req + 34;
+    icmp[0] = 8;
+    for (uint32_t i = 8; i < len - 34; i++) icmp[i] = (uint8_t)(i * 7u + q);
+    const uint16_t cc = csum16(icmp, len - 34);
+    icmp[2] = (uint8_t)(cc >> 8), icmp[3] = (uint8_t)cc;
+    memcpy(rep, req, len);
+    memcpy(rep, src, 6);
+    memcpy(rep + 6, dst, 6);
+    memcpy(rep + 26, ip + 16, 4);
+    memcpy(rep + 30, ip + 12, 4);
+    rep[34] = 0;
+    /* csum_replace2(&csum, 8, 0) on the little-endian-loaded field (xsk_receive.c:101-111) */
+    uint32_t c = (uint32_t)req[36] | (uint32_t)req[37] << 8;
+    c = (~c) & 0xFFFFu;
+    c += (~8u) & 0xFFFFu;
+    c = (c & 0xFFFFu) + (c >> 16);
+    c = (~c) & 0xFFFFu;
+    rep[36] = (uint8_t)c, rep[37] = (uint8_t)(c >> 8);
+}
+
+struct ring_mem { /* one ring: producer, consumer, flags words and the entries */
+    uint32_t prod, cons, flags;
+    void* ents;
+};
+
+static void ring_init(struct xsk_gpu_ring* r, struct ring_mem* m, uint32_t size, size_t esz, int producer_side) {
+    memset(m, 0, sizeof *m);
+    m->ents = calloc(size, esz);
+    memset(r, 0, sizeof *r);
+    r->mask = size - 1;
+    r->size = size;
+    r->producer = &m->prod;
+    r->consumer = &m->cons;
+    r->flags = &m->flags;
+    r->ring = m->ents;
+    if (producer_side) r->cached_cons = size; /* libxdp: a producer's cached consumer is consumer + size */
+}
+
+struct queue {
+    uint32_t q, step, len, ring, frames, empty;
+    int mode, real_mode;
+    double seconds;
+    /* results */
+    uint64_t frames_done, steps, checked, fail;
+    double busy;
+    double* lat;
+    uint64_t nlat;
+    int rc;
+};
+
+static int cmpd(const void* a, const void* b) {
+    const double x = *(const double*)a, y = *(const double*)b;
+    return x < y ? -1 : x > y;
+}
+
+static void* run_queue(void* arg) {
+    struct queue* Q = (struct queue*)arg;
+    const uint32_t R = Q->ring, F = Q->frames, len = Q->len;
+    uint8_t* umem = NULL;
+    if (posix_memalign((void**)&umem, 4096, (size_t)F * CHUNK)) {
+        Q->rc = -12;
+        return NULL;
+    }
+    memset(umem, 0, (size_t)F * CHUNK);
+    uint8_t req[4096], rep[4096];
+    make_pair(req, rep, len, Q->q);
+    struct ring_mem mrx, mfill, mtx, mcomp;
+    struct xsk_gpu_ring rx, fill, tx, comp; /* the application's views */
+    ring_init(&rx, &mrx, R, sizeof(struct xsk_gpu_desc), 0);
+    ring_init(&fill, &mfill, R, 8, 1);
+    ring_init(&tx, &mtx, R, sizeof(struct xsk_gpu_desc), 1);
+    ring_init(&comp, &mcomp, R, 8, 0);
+    struct xsk_gpu_frame_pool pool;
+    pool.addr = (uint64_t*)malloc(sizeof(uint64_t) * F);
+    pool.capacity = F;
+    pool.n_free = 0;
+    for (uint32_t i = 0; i < F; i++) pool.addr[pool.n_free++] = (uint64_t)(F - 1 - i) * CHUNK; /* xsk_utils.c:140-141 */
+    xsk_gpu_ctx* ctx = NULL;
+    const uint32_t maxb = Q->step < XSK_GPU_RX_MAX_STEP ? Q->step : XSK_GPU_RX_MAX_STEP;
+    Q->rc = xsk_gpu_init(&ctx, 0, umem, (uint64_t)F * CHUNK, maxb, Q->mode);
+    if (Q->rc) return NULL;
+    Q->real_mode = xsk_gpu_ctx_mode(ctx);
+    /* the simulated kernel side: its own cursors over the shared index words */
+    uint32_t k_rx_prod = 0, k_fill_cons = 0, k_tx_cons = 0, k_comp_prod = 0;
+    struct xsk_gpu_stats st;
+    memset(&st, 0, sizeof st);
+    const size_t cap = 1u << 22;
+    Q->lat = (double*)malloc(sizeof(double) * cap);
+    /* prime the fill ring (the reference's init, xsk_utils.c:163-177) */
+    {
+        uint32_t idx = 0;
+        const uint32_t n = F < R ? F : R;
+        idx = fill.cached_prod;
+        for (uint32_t i = 0; i < n; i++) ((uint64_t*)mfill.ents)[(idx + i) & (R - 1)] = pool.addr[--pool.n_free];
+        fill.cached_prod += n;
+        __atomic_store_n(&mfill.prod, mfill.prod + n, __ATOMIC_RELEASE);
+    }
+    const double t_end = now_s() + Q->seconds;
+    while (now_s() < t_end && Q->nlat < cap) {
+        /* ---- kernel side (untimed) ---- */
+        const uint32_t tx_prod = __atomic_load_n(&mtx.prod, __ATOMIC_ACQUIRE);
+        for (; k_tx_cons != tx_prod; k_tx_cons++) { /* replies: check every byte, complete */
+            const struct xsk_gpu_desc* d = &((struct xsk_gpu_desc*)mtx.ents)[k_tx_cons & (R - 1)];
+            Q->checked++;
+            if (d->len != len || memcmp(umem + d->addr, rep, len) != 0) Q->fail++;
+            ((uint64_t*)mcomp.ents)[k_comp_prod & (R - 1)] = d->addr;
+            k_comp_prod++;
+        }
+        __atomic_store_n(&mtx.cons, k_tx_cons, __ATOMIC_RELEASE);
+        __atomic_store_n(&mcomp.prod, k_comp_prod, __ATOMIC_RELEASE);
+        const uint32_t fill_prod = __atomic_load_n(&mfill.prod, __ATOMIC_ACQUIRE);
+        const uint32_t rx_cons = __atomic_load_n(&mrx.cons, __ATOMIC_ACQUIRE);
+        uint32_t room = R - (k_rx_prod - rx_cons);
+        if (Q->empty) room = room < Q->step ? room : Q->step; /* exactly one batch per step */
+        for (; room && k_fill_cons != fill_prod; room--, k_fill_cons++) { /* receive a request into each fill frame */
+            const uint64_t base = ((uint64_t*)mfill.ents)[k_fill_cons & (R - 1)] & ~(uint64_t)(CHUNK - 1);
+            memcpy(umem + base + HEADROOM, req, len);
+            struct xsk_gpu_desc* d = &((struct xsk_gpu_desc*)mrx.ents)[k_rx_prod & (R - 1)];
+            d->addr = base + HEADROOM;
+            d->len = len;
+            d->options = 0;
+            k_rx_prod++;
+        }
+        __atomic_store_n(&mfill.cons, k_fill_cons, __ATOMIC_RELEASE);
+        __atomic_store_n(&mrx.prod, k_rx_prod, __ATOMIC_RELEASE);
+        /* ---- the application's loop (timed) ---- */
+        const double t0 = now_s();
+        xsk_gpu_tx_complete(&comp, &pool, R);
+        struct xsk_gpu_rx_result res;
+        const int got = xsk_gpu_rx_step(ctx, &rx, &fill, &tx, &pool, Q->step, &st, &res);
+        const double dt = now_s() - t0;
+        if (got < 0) {
+            Q->rc = got;
+            break;
+        }
+        if (got == 0) continue;
+        if (res.replied != (uint32_t)got || res.tx_full) Q->fail += (uint64_t)got - res.replied;
+        Q->busy += dt;
+        Q->frames_done += (uint64_t)got;
+        Q->steps++;
+        Q->lat[Q->nlat++] = dt;
+    }
+    xsk_gpu_fini(ctx);
+    if (st.rx_packets != Q->frames_done || st.tx_packets != Q->frames_done) Q->fail++;
+    free(umem);
+    free(pool.addr);
+    free(mrx.ents), free(mfill.ents), free(mtx.ents), free(mcomp.ents);
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: %s <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] "
+                        "[frames=4096] [empty=0]\n", argv[0]);
+        return 2;
+    }
+    const uint32_t step = (uint32_t)atoi(argv[1]);
+    const int mode = !strcmp(argv[2], "lowlat") ? XSK_GPU_MODE_LOWLAT
+                     : !strcmp(argv[2], "staged") ? XSK_GPU_MODE_STAGED : XSK_GPU_MODE_ZEROCOPY;
+    const double seconds = atof(argv[3]);
+    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0;
+    for (int a = 4; a < argc; a++) {
+        if (!strncmp(argv[a], "len=", 4)) len = (uint32_t)atoi(argv[a] + 4);
+        else if (!strncmp(argv[a], "queues=", 7)) nq = (uint32_t)atoi(argv[a] + 7);
+        else if (!strncmp(argv[a], "ring=", 5)) ring = (uint32_t)atoi(argv[a] + 5);
+        else if (!strncmp(argv[a], "frames=", 7)) frames = (uint32_t)atoi(argv[a] + 7);
+        else if (!strncmp(argv[a], "empty=", 6)) empty = (uint32_t)atoi(argv[a] + 6);
+    }
+    if (len < 42 || len > CHUNK - HEADROOM || nq < 1 || nq > 16 || (ring & (ring - 1)) || ring < 64 || frames < ring ||
+        step < 1) {
+        fprintf(stderr, "bad arguments\n");
+        return 2;
+    }
+    struct queue Q[16];
+    pthread_t th[16];
+    memset(Q, 0, sizeof Q);
+    for (uint32_t q = 0; q < nq; q++) {
+        Q[q].q = q;
+        Q[q].step = step;
+        Q[q].len = len;
+        Q[q].ring = ring;
+        Q[q].frames = frames;
+        Q[q].empty = empty;
+        Q[q].mode = mode;
+        Q[q].seconds = seconds;
+        pthread_create(&th[q], NULL, run_queue, &Q[q]);
+    }
+    uint64_t tot = 0, checked = 0, fail = 0;
+    double busy_max = 0.0;
+    int rc = 0;
+    printf("{\"tool\": \"rxring\", \"step\": %u, \"mode\": \"%s\", \"len\": %u, \"queues\": %u, \"ring\": %u, "
+           "\"frames\": %u, \"empty\": %u, \"per_queue\": [", step, argv[2], len, nq, ring, frames, empty);
+    for (uint32_t q = 0; q < nq; q++) {
+        pthread_join(th[q], NULL);
+        struct queue* R = &Q[q];
+        if (R->rc) rc = R->rc;
+        qsort(R->lat, R->nlat, sizeof(double), cmpd);
+        const double p50 = R->nlat ? R->lat[R->nlat / 2] : 0.0, p99 = R->nlat ? R->lat[(R->nlat * 99) / 100] : 0.0;
+        printf("%s{\"mode\": %d, \"mframes_s\": %.3f, \"us_per_step\": %.3f, \"p50_us\": %.3f, \"p99_us\": %.3f, "
+               "\"frames_per_step\": %.1f, \"steps\": %llu, \"rc\": %d}", q ? ", " : "", R->real_mode,
+               R->busy > 0 ? 1e-6 * (double)R->frames_done / R->busy : 0.0,
+               R->steps ? 1e6 * R->busy / (double)R->steps : 0.0, 1e6 * p50, 1e6 * p99,
+               R->steps ? (double)R->frames_done / (double)R->steps : 0.0, (unsigned long long)R->steps, R->rc);
+        tot += R->frames_done;
+        checked += R->checked;
+        fail += R->fail;
+        if (R->busy > busy_max) busy_max = R->busy;
+        free(R->lat);
+    }
+    printf("], \"mframes_s_total\": %.3f, \"frames\": %llu, \"checked\": %llu, \"failures\": %llu, \"rc\": %d}\n",
+           busy_max > 0 ? 1e-6 * (double)tot / busy_max : 0.0, (unsigned long long)tot, (unsigned long long)checked,
+           (unsigned long long)fail, rc);
+    return rc || fail ? 1 : 0;
+}

@@ -80,6 +80,8 @@ struct xsk_gpu_ctx {
     int registered;   /* this context registered the UMEM (and unregisters it at fini) */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
+    uint64_t ll_outcome[3]; /* LOWLAT doorbell batches that timed out: all, completed through the launch path after a
+                             * partial service, returned -ETIMEDOUT (xsk_gpu__lowlat_outcomes) */
 };
 
 /* LOWLAT contexts per device in this process (include/xsk_gpu.h, XSK_GPU_LOWLAT_PER_DEVICE): a slot is taken at
@@ -325,6 +327,11 @@ int xsk_gpu__staged_noalias(xsk_gpu_ctx* c, uint32_t half_bytes) {
     return 0;
 }
 int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
+int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[3]) {
+    if (!c || !out || !c->ll) return -EINVAL;
+    for (int i = 0; i < 3; i++) out[i] = c->ll_outcome[i];
+    return 0;
+}
 xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
 
 int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
@@ -520,6 +527,7 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
          * completes, every frame transformed exactly once */
         const int partial = rc == -ETIMEDOUT && !xsk_gpu__lowlat_broken(c->ll) && unserved &&
                             unserved != (1u << w) - 1u;
+        if (rc == -ETIMEDOUT) c->ll_outcome[partial ? 1 : 2]++, c->ll_outcome[0]++;
         if (rc && !partial) return rc;
         uint8_t hv[XSK_GPU_LOWLAT_MAX];
         memcpy(hv, xsk_gpu__lowlat_verdicts(c->ll), n);

@@ -190,6 +190,10 @@ int xsk_gpu__lowlat_trace(xsk_gpu_ctx* ctx, uint64_t out_ns[15]);
  * microseconds (0 = 2 s).  -EINVAL for a non-LOWLAT context or values out of range. */
 int xsk_gpu__lowlat_tune(xsk_gpu_ctx* ctx, uint32_t tile_frames, uint32_t groups, uint32_t timeout_us);
 XSK_GPU__HIDDEN xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* ctx);
+/* xsk_gpu_host.c (exported for the GPU tests, not part of the ABI): a LOWLAT context's doorbell batches that missed their
+ * completion timeout since init -- out[0] all of them, out[1] those completed through the launch path after the
+ * resident grid had served part of them, out[2] those returned as -ETIMEDOUT.  -EINVAL for other modes. */
+int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* ctx, uint64_t out[3]);
 
 #ifdef __cplusplus
 }
