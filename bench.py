@@ -336,8 +336,13 @@ def host_inclusive_multi(cfg, world, budget_s=2.0, n=1 << 18):
                     t += time.perf_counter() - t0
                     reps += 1
                     ok = ok and bool((v == X.TX_REPLY).all()) and int(st["tx_packets"]) == n
+                # every context's copy-in record (xsk_gpu__staged_stats): bytes moved host -> device and the path
+                # each chunk took -- a context without a device alias of the UMEM shows up as host-pack chunks
+                staged = ctx.staged_stats()
             out[f"g{g}"] = {"gpus": g, "mframes_per_s": round(reps * n / t / 1e6, 3),
-                            "gib_per_s": round(reps * nbytes / t / 2**30, 3), "calls": reps, "verified": ok}
+                            "gib_per_s": round(reps * nbytes / t / 2**30, 3), "calls": reps, "verified": ok,
+                            "staged_stats": staged,
+                            "h2d_per_frame_byte": round(sum(x["h2d_bytes"] for x in staged) / ((reps + 1) * nbytes), 4)}
     except Exception as e:  # noqa: BLE001 -- context only: the bench line must not depend on it
         out["error"] = f"{type(e).__name__}: {e}"
     return out

@@ -421,40 +421,43 @@ def test_lowlat_timeout_exactly_once():
 
 
 def test_lowlat_partial_timeout_deterministic():
-    """the partly-served timeout path, made to happen.  A hog kernel holds every CU for 300 ms except one on
-    each even XCC (released after 1 ms), then a LOWLAT call posts 1024 x 1500-B frames to a fresh resident grid of four
-    workgroups with a 20-ms timeout: the grid's workgroups go round-robin over four consecutive XCCs, so two of them find
-    a CU and serve their slices and two wait behind the hog.  At the timeout the call posts STOP and waits for the grid; when the hog ends, 2 and 3 start, find STOP and
-    retire their slices unserved -- so the call finishes those two slices through the launch path and returns 0.  The
-    output must be exactly the oracle's, and the context must count the batch as a partial completion."""
+    """the partly-served timeout path, made to happen.  The resident grid is launched with two workgroups
+    (test switch) while a 1024 x 1500-B batch is posted for four: slices 0 and 1 are served, 2 and 3 never are.  At the
+    20-ms timeout the call posts STOP, the two workgroups leave, the host finds slices 2 and 3 untouched and finishes them
+    through the launch path: the call returns 0, every byte, verdict, record and counter is the oracle's, and the context
+    counts the batch as a partial completion.  Then the grid at full width serves the next batch normally."""
     _dev()
     n = 1024
     umem = np.zeros(n * 2048, np.uint8)
-    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED6161, mode=0, len_lo=1500, len_hi=1500)
+    descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED6161, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
-    ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    hog = torch.cuda.Stream()
     work = umem.copy()
     with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_LOWLAT) as ctx:
         assert ctx.mode == X.MODE_LOWLAT
         ctx.lowlat_tune(groups=4, timeout_us=20000)
-        claim = torch.zeros(8, dtype=torch.int32, device="cuda:0")
-        torch.cuda.synchronize()
-        assert X.tune_lib().xsk_gpu__test_hog(ncu, 300000, 0x55, claim.data_ptr(), hog.cuda_stream) == 0
-        time.sleep(0.01)  # the hog's workgroups are resident, the early ones gone
+        ctx.lowlat_test_width(2)
         v, r, st = ctx.process(descs)
         out = ctx.lowlat_outcomes()
-        hog.synchronize()
-        print("hog claims per XCC:", claim.tolist(), "outcomes:", out)
-        assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
-        assert int(st["tx_packets"]) == int(s_ref["tx_packets"]) and int(st["rx_bytes"]) == int(s_ref["rx_bytes"])
         assert out == {"timeouts": 1, "partial": 1, "untouched": 0}, out
-        # the context works on afterwards (its grid relaunched by the next batch)
+        assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
+        for k in COUNTERS:
+            assert int(st[k]) == int(s_ref[k]), k
+        # one workgroup for a 256-frame batch posted over four slices: slice 0 served, slices 1-3 by the launch path
+        ctx.lowlat_test_width(1)
+        work[:] = umem
+        mid = np.ascontiguousarray(descs[256:512])
+        ref2 = umem.copy()
+        v2_ref, r2_ref, _ = oracle.echo_batch(ref2, mid)
+        v, r, _ = ctx.process(mid)
+        assert ctx.lowlat_outcomes() == {"timeouts": 2, "partial": 2, "untouched": 0}
+        assert (v == v2_ref).all() and (r == r2_ref).all() and (work == ref2).all()
+        ctx.lowlat_test_width(0)
         ctx.lowlat_tune(groups=0, timeout_us=0)
         work[:] = umem
-        v, r, _ = ctx.process(descs)
-        assert (v == v_ref).all() and (work == ref).all()
+        v, r, st = ctx.process(descs)
+        assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
+        assert ctx.lowlat_outcomes()["timeouts"] == 2
 
 
 def test_lowlat_reserved_queue_for_an_application_stream():

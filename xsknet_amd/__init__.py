@@ -126,13 +126,13 @@ _SIGS = {
     "xsk_gpu__staged_stats": ([_P, C.POINTER(C.c_uint64)], C.c_int),
     "xsk_gpu__staged_noalias": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu__lowlat_outcomes": ([_P, C.POINTER(C.c_uint64)], C.c_int),
+    "xsk_gpu__lowlat_test_width": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu__multi_ctx": ([_P, C.c_uint32], _P),
     # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
     "xsk_gpu__echo_dev_grid": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32], C.c_int),
 }
 _TUNE_SIGS = {
     "xsk_gpu__product_variant": ([C.c_int, C.c_uint32, _P, C.c_uint64, _P, C.c_uint32, _P, _P, _P, _P], C.c_int),
-    "xsk_gpu__test_hog": ([C.c_uint32, C.c_uint32, C.c_uint32, _P, _P], C.c_int),
 }
 _tune: Optional[C.CDLL] = None
 
@@ -328,6 +328,10 @@ class EchoContext:
         """Tool / test knobs of a LOWLAT context (xsk_gpu__lowlat_tune): frames per wave, serving workgroups,
         completion timeout (0 = defaults)."""
         _check("xsk_gpu__lowlat_tune", lib().xsk_gpu__lowlat_tune(self._ctx, tile_frames, groups, timeout_us))
+
+    def lowlat_test_width(self, wgs: int) -> None:
+        """Test switch (xsk_gpu__lowlat_test_width): launch the resident grid with `wgs` workgroups (0 = all)."""
+        _check("xsk_gpu__lowlat_test_width", lib().xsk_gpu__lowlat_test_width(self._ctx, wgs))
 
     def lowlat_outcomes(self):
         """xsk_gpu__lowlat_outcomes: doorbell batches that missed their timeout -- all, completed through the launch

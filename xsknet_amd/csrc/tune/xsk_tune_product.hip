@@ -425,34 +425,6 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
     return 0;
 }
 
-// Test aid (tests/test_gpu_staged.py::test_lowlat_partial_timeout_deterministic): `wgs` workgroups that each hold a
-// whole CU (96 KiB of LDS) for `usec` microseconds of wall clock, sleeping, except ONE workgroup on each XCC whose id is
-// in the bit mask `early_xcc` (the first to claim its XCC's slot in d_claim[8], zeroed), which leaves after 1 ms.  A grid
-// launched meanwhile finds free CUs only on those XCCs: workgroups are placed on the XCCs round-robin, so a 4-workgroup
-// grid placed on four consecutive XCCs finds exactly two free CUs when the mask holds every other XCC, whatever XCC
-// its round-robin starts at.  Bounded by the clock: it always ends.
-__global__ __launch_bounds__(64) void hog_kernel(uint64_t ticks, uint32_t early_xcc, uint32_t* claim) {
-    __shared__ volatile uint32_t big[96 * 256];
-    const uint64_t t0 = wall_clock64();
-    big[threadIdx.x] = (uint32_t)t0;
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7u;
-    __shared__ uint32_t early;
-    if (threadIdx.x == 0) early = ((early_xcc >> xcc) & 1u) && atomicAdd(claim + xcc, 1u) == 0u;
-    __syncthreads();
-    const uint64_t lim = early ? 100000u : ticks;  // 100-MHz wall clock: 1 ms
-    while (wall_clock64() - t0 < lim) __builtin_amdgcn_s_sleep(100);
-    if (big[threadIdx.x] == 0xFFFFFFFFu) big[0] = 0;
-}
-
-extern "C" int xsk_gpu__test_hog(uint32_t wgs, uint32_t usec, uint32_t early_xcc, void* d_claim, void* stream) {
-    if (wgs == 0 || wgs > 4096 || usec > 2000000u || !d_claim) return -EINVAL;
-    hog_kernel<<<dim3(wgs), dim3(64), 0, (hipStream_t)stream>>>((uint64_t)usec * 100u, early_xcc, (uint32_t*)d_claim);
-    HIP_TRY(hipGetLastError());
-    return 0;
-}
-
 // The tuning library's own copy of the error hook (the product library's is hidden).
 extern "C" __attribute__((visibility("hidden"))) int xsk_gpu__hip_fail(hipError_t e) {
     return e == hipErrorOutOfMemory ? -ENOMEM : -EIO;

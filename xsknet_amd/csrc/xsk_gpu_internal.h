@@ -194,6 +194,11 @@ XSK_GPU__HIDDEN xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* ctx);
  * completion timeout since init -- out[0] all of them, out[1] those completed through the launch path after the
  * resident grid had served part of them, out[2] those returned as -ETIMEDOUT.  -EINVAL for other modes. */
 int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* ctx, uint64_t out[3]);
+/* xsk_lowlat.hip (test switch, not part of the ABI): the resident grid is launched with `wgs` workgroups (1 ..
+ * XSK_GPU__LL_WG; 0 = all) from the next batch on, while batches are still posted for as many workgroups as their size
+ * asks (xsk_gpu__lowlat_tune's `groups`): slices of workgroups that do not exist are never served, which makes a batch
+ * time out partly served -- the deterministic test of the partial-timeout path. */
+int xsk_gpu__lowlat_test_width(xsk_gpu_ctx* ctx, uint32_t wgs);
 
 #ifdef __cplusplus
 }

@@ -310,6 +310,7 @@ struct xsk_gpu__lowlat {
     uint32_t tile_q;       // frames per wave / 4 (0: from the slice's bytes); xsk_gpu__lowlat_tune
     uint32_t groups;       // serving workgroups (0: xsk_gpu__ll_groups); xsk_gpu__lowlat_tune
     uint64_t host_ns[2];   // last batch on the host: entry -> doorbell posted, posted -> completion seen
+    uint32_t width;        // workgroups a launch starts (0: XSK_GPU__LL_WG); xsk_gpu__lowlat_test_width
 };
 
 static int ll_launch(void* u) {
@@ -319,10 +320,11 @@ static int ll_launch(void* u) {
     const uint64_t c = __atomic_load_n(&ll->h_bell->cmd, __ATOMIC_SEQ_CST);
     if (c & XSK_GPU__BELL_STOP) xsk_gpu__ll_post(ll->h_bell, c & ~XSK_GPU__BELL_STOP);
     ll->args.gen++;
+    const dim3 grid(ll->width ? ll->width : XSK_GPU__LL_WG);
     if (ll->args.opts)
-        hipLaunchKernelGGL(lowlat_kernel<true>, dim3(XSK_GPU__LL_WG), dim3(kThreads6), 0, ll->stream, ll->args);
+        hipLaunchKernelGGL(lowlat_kernel<true>, grid, dim3(kThreads6), 0, ll->stream, ll->args);
     else
-        hipLaunchKernelGGL(lowlat_kernel<false>, dim3(XSK_GPU__LL_WG), dim3(kThreads6), 0, ll->stream, ll->args);
+        hipLaunchKernelGGL(lowlat_kernel<false>, grid, dim3(kThreads6), 0, ll->stream, ll->args);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -498,6 +500,14 @@ int xsk_gpu__lowlat_tune(xsk_gpu_ctx* ctx, uint32_t tile_frames, uint32_t groups
     ll->tile_q = tile_frames / 4u;
     ll->groups = groups;
     ll->st.timeout_s = timeout_us ? 1e-6 * (double)timeout_us : 2.0;
+    return 0;
+}
+
+int xsk_gpu__lowlat_test_width(xsk_gpu_ctx* ctx, uint32_t wgs) {
+    xsk_gpu__lowlat* ll = xsk_gpu__ctx_lowlat(ctx);
+    if (!ll || wgs > XSK_GPU__LL_WG) return -EINVAL;
+    xsk_gpu__lowlat_stop(ll);  // the next batch launches a grid of the new width
+    ll->width = wgs;
     return 0;
 }
 
