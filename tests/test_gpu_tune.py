@@ -15,9 +15,9 @@ import xsknet_amd as X  # noqa: E402
 
 # 0 as shipped (reference), 2 wire mode as shipped, 5 / 6 no SPLIT
 # (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4, 22 / 23 wire as shipped with VLAN only /
-# SLACK 0.  (Round 5 removed 14-18, 21 and 24 with their switches from the product header: RS 2, LASTW, the 128-B wire
+# SLACK 0, 42 HB (the header phase's window read with b128 LDS reads).  (Round 5 removed 14-18, 21 and 24 with their switches from the product header: RS 2, LASTW, the 128-B wire
 # windows and unpaired wire tiles, each lost in a committed A/B log.)
-VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 22, 23]
+VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 22, 23, 42]
 WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL}
 # the short-tile grids of round 5 (tune/xsk_tune_product.hip SG / SGP, c2 experiments): they handle all-short batches
 # only, so they are checked on one (every tile pair short), every byte against the oracle

@@ -9,11 +9,13 @@ run() { local name=$1 to=$2; shift 2
   echo "== $name $(date +%T)"; timeout -k 10 "$to" "$@" > "$O/$name.log" 2>&1; local rc=$?
   echo "rc=$rc"; tail -1 "$O/$name.log" | cut -c1-300; return $rc; }
 SQ="SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_WAIT_INST_ANY,SQ_WAIT_ANY,SQ_WAVE_CYCLES"
-declare -A ALG=([c3]=1572864000 [c4]=819879113 [c2]=67108864 [c3_opts7]=1572864000)
-# c3_opts7: c3 in wire mode (bench.py --opts 7 reads profiles/traffic_c3_opts7.json)
-for c in c3 c4 c2 c3_opts7; do
+declare -A ALG=([c3]=1572864000 [c4]=819879113 [c2]=67108864 [c3_opts7]=1572864000 [c5]=1572864000)
+# c3_opts7: c3 in wire mode (bench.py --opts 7 reads profiles/traffic_c3_opts7.json); c5: per launch of 1 M frames (a
+# call is 64 such launches over consecutive slices of its descriptors)
+for c in c3 c4 c2 c3_opts7 c5; do
   cfg=${c%_opts7}; X=""; [ "$c" != "$cfg" ] && X="--opts 7"
-  B="python3 $GRAFT_REPO_ROOT/bench.py --config $cfg $X --steps 4 --warmup 1 --no-cpu"
+  S="--steps 4 --warmup 1"; [ "$c" = c5 ] && S="--steps 1 --warmup 1"
+  B="python3 $GRAFT_REPO_ROOT/bench.py --config $cfg $X $S --no-cpu"
   run pmc_fetch_$c 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc_fetch_$c -o run -- $B || exit 1
   run pmc_write_$c 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc_write_$c -o run -- $B || exit 1
   run pmc_sq_$c 240 rocprofv3 --pmc $SQ --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/pmc_sq_$c -o run -- $B || exit 1

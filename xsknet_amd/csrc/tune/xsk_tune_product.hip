@@ -80,84 +80,6 @@ __global__ __launch_bounds__(kThreads6, 1) void timed_round_kernel(EchoArgs a, u
     }
 }
 
-// SG (round 5, VERDICT r04 next #3): c2's all-short batches on a NON-persistent grid of small workgroups -- WPB waves
-// each, every wave one pair of short tiles (read_round_short2: both descriptor loads, then all eight frame loads, the
-// header phase of each tile), written as soon as the wave has read (no rounds, no arrival counter).  The upper bound of
-// the idea: a tile with a longer frame is not processed (its verdicts stay as they were; outputs_equal_shipped flags
-// it), so it is only measured on all-short batches.  WT: windows and records stored write-through as in the product.
-template <bool WIRE, int WPB, bool WT>
-__global__ __launch_bounds__(WPB * 64) void short_grid_kernel(EchoArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t hdr[WPB][2][kTile * kWin];
-    __shared__ uint32_t sums[WPB][2][kTile];
-    __shared__ unsigned long long cnts[WPB][4];
-    const uint32_t wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
-    const uint32_t t0 = 2u * (blockIdx.x * (uint32_t)WPB + wave);
-    Counters cnt;
-    if (t0 + 1u < ntiles) {  // wave-uniform (the batch is a whole number of tile pairs in the A/B)
-        u32x4 rec[2];
-        uint32_t verd[2], alo[2], ahi[2], round_long = 0;
-        uint64_t wbm[2];
-        if (read_round_short2<kRefHeavy, WIRE>(a, t0, t0 + 1u, hdr[wave][0], hdr[wave][1], sums[wave][0], sums[wave][1],
-                                              lane, cnt, rec, verd, alo, ahi, wbm, round_long)) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const uint32_t t = t0 + (uint32_t)i;
-                const uint8_t* rows = hdr[wave][i];
-                if (wbm[i]) {
-                    const uint32_t hi_u = WT ? rdlane(ahi[i], (uint32_t)__builtin_ctzll(wbm[i])) : 0u;
-                    const bool wt_tile = WT && __ballot(((wbm[i] >> lane) & 1ull) &&
-                                                        (ahi[i] != hi_u || alo[i] > 0xFFFFFFC0u)) == 0ull;
-                    const __amdgpu_buffer_rsrc_t wrs =
-                        __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + ((uint64_t)hi_u << 32)), (short)0, -1, kRsrcFlags);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
-                        const uint32_t kk = lane & 3u;
-                        const uint32_t flo = (uint32_t)__shfl((int)alo[i], (int)f, 64);
-                        const uint32_t fhi = (uint32_t)__shfl((int)ahi[i], (int)f, 64);
-                        if ((wbm[i] >> f) & 1ull) {
-                            const u32x4 w = *(const u32x4*)(rows + f * kWin + 16u * kk);
-                            if (WT && wt_tile) __builtin_amdgcn_raw_buffer_store_b128(w, wrs, (int)(flo + 16u * kk), 0, kAuxSC1);
-                            else *(u32x4*)(a.umem + ((uint64_t)flo | ((uint64_t)fhi << 32)) + 16u * kk) = w;
-                        }
-                    }
-                }
-                const uint32_t fi = t * (uint32_t)kTile + lane;
-                if (fi < a.n) {
-                    if (a.recs) {
-                        if (WT)
-                            __builtin_amdgcn_raw_buffer_store_b128(
-                                rec[i], __builtin_amdgcn_make_buffer_rsrc((void*)((u32x4*)a.recs + (uint64_t)t * kTile), (short)0, -1, kRsrcFlags),
-                                (int)(lane * 16u), 0, kAuxSC1);
-                        else ((u32x4*)a.recs)[fi] = rec[i];
-                    }
-                    if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[i];
-                }
-            }
-        }
-    }
-    // counters: one partial row per workgroup (the A/B's workspace holds 32 768 rows)
-    cnt.rxp = wave_sum_u64(cnt.rxp);
-    cnt.rxb = wave_sum_u64(cnt.rxb);
-    cnt.txp = wave_sum_u64(cnt.txp);
-    cnt.txb = wave_sum_u64(cnt.txb);
-    if (lane == 0) {
-        cnts[wave][0] = cnt.rxp;
-        cnts[wave][1] = cnt.rxb;
-        cnts[wave][2] = cnt.txp;
-        cnts[wave][3] = cnt.txb;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (threadIdx.x < 4 && a.partials) {
-        unsigned long long s = 0;
-#pragma unroll
-        for (int w = 0; w < WPB; ++w) s += cnts[w][threadIdx.x];
-        a.partials[blockIdx.x * 4 + threadIdx.x] = s;
-    }
-}
-
 // SGP (round 5): the SG kernel with every wave looping over PPW tile pairs in a two-deep software pipeline -- pair p + 1's
 // frame loads and pair p + 2's descriptor loads are issued before pair p's header phase and stores, so no load waits
 // behind this wave's earlier stores (vmcnt counts loads and stores in one in-order counter).  The pair's descriptors,
@@ -283,6 +205,136 @@ __device__ __forceinline__ void sg_finish_store(const EchoArgs& a, const SgPair&
     __builtin_amdgcn_wave_barrier();  // rows / sums are rewritten by the next pair
 }
 
+// SG (round 5, VERDICT r04 next #3): c2's all-short batches on a NON-persistent grid of small workgroups -- WPB waves
+// each, every wave one pair of short tiles (read_round_short2: both descriptor loads, then all eight frame loads, the
+// header phase of each tile), written as soon as the wave has read (no rounds, no arrival counter).  The upper bound of
+// the idea: a tile with a longer frame is not processed (its verdicts stay as they were; outputs_equal_shipped flags
+// it), so it is only measured on all-short batches.  WT: windows and records stored write-through as in the product.
+// DIAG (diagnostics, wrong outputs): 1 = no header phase (windows stored as read, records zero); 2 = no LDS either --
+// each quad of lanes stores the 64 bytes it loaded straight back, c2floor mode 3's traffic in this kernel's skeleton.
+template <bool WIRE, int WPB, bool WT, int DIAG = 0>
+__global__ __launch_bounds__(WPB * 64) void short_grid_kernel(EchoArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t hdr[WPB][2][kTile * kWin];
+    __shared__ uint32_t sums[WPB][2][kTile];
+    __shared__ unsigned long long cnts[WPB][4];
+    const uint32_t wave = uniform(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t ntiles = (a.n + kTile - 1) / kTile;
+    const uint32_t t0 = 2u * (blockIdx.x * (uint32_t)WPB + wave);
+    Counters cnt;
+    if (t0 + 1u < ntiles) {  // wave-uniform (the batch is a whole number of tile pairs in the A/B)
+        u32x4 rec[2];
+        uint32_t verd[2], alo[2], ahi[2], round_long = 0;
+        uint64_t wbm[2];
+        if (DIAG) {
+            SgPair S;
+            sg_desc(a, t0, lane, S);
+            const bool ok = sg_frames<WIRE>(a, lane, S);
+            if (DIAG == 2 && ok) {  // straight back, 4 lanes per frame
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    const u32x4 dd = tt ? S.d1 : S.d0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                        const uint32_t flo = (uint32_t)__shfl((int)dd.x, (int)f, 64);
+                        const uint32_t fhi = (uint32_t)__shfl((int)dd.y, (int)f, 64);
+                        *(u32x4*)(a.umem + ((uint64_t)flo | ((uint64_t)fhi << 32)) + 16u * (lane & 3u)) = tt ? S.x1[r] : S.x0[r];
+                    }
+                    const uint32_t fi = (t0 + (uint32_t)tt) * (uint32_t)kTile + lane;
+                    if (fi < a.n) {
+                        if (a.recs) ((u32x4*)a.recs)[fi] = dd;
+                        if (a.verdicts) a.verdicts[fi] = 0;
+                    }
+                }
+            } else if (ok) {  // through LDS, no header phase
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    uint8_t* rows = hdr[wave][tt];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        *(u32x4*)(rows + ((uint32_t)r * 16u + (lane >> 2)) * kWin + 16u * (lane & 3u)) = tt ? S.x1[r] : S.x0[r];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    const u32x4 dd = tt ? S.d1 : S.d0;
+                    const uint8_t* rows = hdr[wave][tt];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                        const uint32_t flo = (uint32_t)__shfl((int)dd.x, (int)f, 64);
+                        const uint32_t fhi = (uint32_t)__shfl((int)dd.y, (int)f, 64);
+                        const u32x4 w = *(const u32x4*)(rows + f * kWin + 16u * (lane & 3u));
+                        *(u32x4*)(a.umem + ((uint64_t)flo | ((uint64_t)fhi << 32)) + 16u * (lane & 3u)) = w;
+                    }
+                    const uint32_t fi = (t0 + (uint32_t)tt) * (uint32_t)kTile + lane;
+                    if (fi < a.n) {
+                        if (a.recs) ((u32x4*)a.recs)[fi] = dd;
+                        if (a.verdicts) a.verdicts[fi] = 0;
+                    }
+                }
+            }
+        } else if (read_round_short2<kRefHeavy, WIRE>(a, t0, t0 + 1u, hdr[wave][0], hdr[wave][1], sums[wave][0], sums[wave][1],
+                                              lane, cnt, rec, verd, alo, ahi, wbm, round_long)) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t t = t0 + (uint32_t)i;
+                const uint8_t* rows = hdr[wave][i];
+                if (wbm[i]) {
+                    const uint32_t hi_u = WT ? rdlane(ahi[i], (uint32_t)__builtin_ctzll(wbm[i])) : 0u;
+                    const bool wt_tile = WT && __ballot(((wbm[i] >> lane) & 1ull) &&
+                                                        (ahi[i] != hi_u || alo[i] > 0xFFFFFFC0u)) == 0ull;
+                    const __amdgpu_buffer_rsrc_t wrs =
+                        __builtin_amdgcn_make_buffer_rsrc((void*)(a.umem + ((uint64_t)hi_u << 32)), (short)0, -1, kRsrcFlags);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t f = (uint32_t)r * 16u + (lane >> 2);
+                        const uint32_t kk = lane & 3u;
+                        const uint32_t flo = (uint32_t)__shfl((int)alo[i], (int)f, 64);
+                        const uint32_t fhi = (uint32_t)__shfl((int)ahi[i], (int)f, 64);
+                        if ((wbm[i] >> f) & 1ull) {
+                            const u32x4 w = *(const u32x4*)(rows + f * kWin + 16u * kk);
+                            if (WT && wt_tile) __builtin_amdgcn_raw_buffer_store_b128(w, wrs, (int)(flo + 16u * kk), 0, kAuxSC1);
+                            else *(u32x4*)(a.umem + ((uint64_t)flo | ((uint64_t)fhi << 32)) + 16u * kk) = w;
+                        }
+                    }
+                }
+                const uint32_t fi = t * (uint32_t)kTile + lane;
+                if (fi < a.n) {
+                    if (a.recs) {
+                        if (WT)
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                rec[i], __builtin_amdgcn_make_buffer_rsrc((void*)((u32x4*)a.recs + (uint64_t)t * kTile), (short)0, -1, kRsrcFlags),
+                                (int)(lane * 16u), 0, kAuxSC1);
+                        else ((u32x4*)a.recs)[fi] = rec[i];
+                    }
+                    if (a.verdicts) a.verdicts[fi] = (uint8_t)verd[i];
+                }
+            }
+        }
+    }
+    // counters: one partial row per workgroup (the A/B's workspace holds 32 768 rows)
+    cnt.rxp = wave_sum_u64(cnt.rxp);
+    cnt.rxb = wave_sum_u64(cnt.rxb);
+    cnt.txp = wave_sum_u64(cnt.txp);
+    cnt.txb = wave_sum_u64(cnt.txb);
+    if (lane == 0) {
+        cnts[wave][0] = cnt.rxp;
+        cnts[wave][1] = cnt.rxb;
+        cnts[wave][2] = cnt.txp;
+        cnts[wave][3] = cnt.txb;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (threadIdx.x < 4 && a.partials) {
+        unsigned long long s = 0;
+#pragma unroll
+        for (int w = 0; w < WPB; ++w) s += cnts[w][threadIdx.x];
+        a.partials[blockIdx.x * 4 + threadIdx.x] = s;
+    }
+}
+
 template <bool WIRE, int WPB, int PPW, bool PERSIST>
 __global__ __launch_bounds__(WPB * 64) void short_pipe_kernel(EchoArgs a, uint32_t pairs_per_wg) {
     __shared__ __attribute__((aligned(16))) uint8_t hdr[WPB][2][kTile * kWin];
@@ -349,12 +401,12 @@ static int short_pipe(const EchoArgs& args, hipStream_t s, uint32_t ncu) {
     return 0;
 }
 
-template <bool WIRE, int WPB, bool WT>
+template <bool WIRE, int WPB, bool WT, int DIAG = 0>
 static int short_grid(const EchoArgs& args, hipStream_t s) {
     const uint32_t pairs = (args.n + 2 * kTile - 1) / (2 * kTile);
     const uint32_t grid = (pairs + WPB - 1) / WPB;
     if (grid > 32768u) return -EINVAL;  // partial rows in the A/B's 1 MiB workspace
-    short_grid_kernel<WIRE, WPB, WT><<<dim3(grid), dim3(WPB * 64), 0, s>>>(args);
+    short_grid_kernel<WIRE, WPB, WT, DIAG><<<dim3(grid), dim3(WPB * 64), 0, s>>>(args);
     return 0;
 }
 
@@ -415,6 +467,12 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         case 37: if (short_pipe<false, 4, 2, false>(args, s, 0)) return -EINVAL; break;
         case 38: if (short_pipe<false, 4, 4, false>(args, s, 0)) return -EINVAL; break;
         case 39: if (short_pipe<false, 8, 2, false>(args, s, 0)) return -EINVAL; break;
+        // 40 / 41: diagnostics (wrong outputs): SG without the header phase / without LDS and header phase
+        case 40: if (short_grid<false, 4, true, 1>(args, s)) return -EINVAL; break;
+        case 41: if (short_grid<false, 4, true, 2>(args, s)) return -EINVAL; break;
+        // 42: HB -- the reference header phase's window read as three ds_read_b128 (aligned waves) and an aligned
+        // reply's patch stored as two b128 + one b64
+        case 42: echo_round_kernel<false, false, kUR, true, true, kRefSlack, true><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

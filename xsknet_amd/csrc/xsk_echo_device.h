@@ -445,14 +445,26 @@ __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc,
 // patched in LDS and returns true (the caller stores the whole window), any other reply is written here,
 // byte-exact.
 // ================================================================================================
+// HB (tuning switch, round 5): a wave whose frames all start 16-B aligned reads its window's first 48 bytes with three
+// ds_read_b128 instead of eleven ds_read_b32 -- the rows are 64 B apart, so a b32 read of one dword in every row meets
+// 16 lanes on each of two banks (16-way), a b128 read 4-way -- and an aligned reply's patch goes back as two b128 and one
+// b64 store instead of seven b32 ones (the unchanged dwords 3-5 rewritten with the values read).
+template <bool HB = false>
 __device__ __forceinline__ bool header_phase_ref(const EchoArgs& a, uint8_t* row, uint32_t ic_raw, uint64_t addr,
                                                  uint32_t len, bool live, bool ok, bool parse, Counters& cnt,
                                                  u32x4* rec_out, uint32_t* verd_out) {
     const uint32_t off = (uint32_t)addr & 15u;
-    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
     uint32_t h[10];  // frame-relative dwords: h[k] = bytes [4k, 4k+4) of the frame
+    const bool hb = HB && __ballot(off != 0u) == 0ull;  // wave-uniform
+    if (hb) {
+        const u32x4 q0 = *(const u32x4*)row, q1 = *(const u32x4*)(row + 16), q2 = *(const u32x4*)(row + 32);
+        h[0] = q0.x, h[1] = q0.y, h[2] = q0.z, h[3] = q0.w, h[4] = q1.x, h[5] = q1.y, h[6] = q1.z, h[7] = q1.w;
+        h[8] = q2.x, h[9] = q2.y;
+    } else {
+        const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
 #pragma unroll
-    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+        for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+    }
 
     // parsed fields (xsk_receive.c:135,140,144,157)
     const uint32_t eth_proto = parse ? (((h[3] & 0xFFu) << 8) | ((h[3] >> 8) & 0xFFu)) : 0u;
@@ -510,13 +522,20 @@ __device__ __forceinline__ bool header_phase_ref(const EchoArgs& a, uint8_t* row
         const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
         if (off == 0 && a.umem_size - addr >= (uint64_t)kWin) {
             uint32_t* r32 = (uint32_t*)row;  // patched in LDS, stored as a whole window by the caller
-            r32[0] = n0;
-            r32[1] = n1;
-            r32[2] = n2;
-            r32[6] = n6;
-            r32[7] = n7;
-            r32[8] = n8;
-            r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+            if (HB) {
+                *(u32x4*)row = u32x4{n0, n1, n2, h[3]};
+                *(u32x4*)(row + 16) = u32x4{h[4], h[5], n6, n7};
+                r32[8] = n8;
+                r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+            } else {
+                r32[0] = n0;
+                r32[1] = n1;
+                r32[2] = n2;
+                r32[6] = n6;
+                r32[7] = n7;
+                r32[8] = n8;
+                r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+            }
             wb = true;
         } else {
             uint8_t* pkt = a.umem + addr;
@@ -815,7 +834,7 @@ __device__ __forceinline__ FrameIn frame_in(const EchoArgs& a, u32x4 dsc, bool i
 // round pays two memory round trips instead of four, with twice the bytes in flight.  The windows go to the
 // two LDS slots, the ICMP sums to the two sum rows, then the header phase of each tile.  Returns false
 // (nothing written) when either tile has a longer frame.
-template <int HEAVY, bool WIRE>
+template <int HEAVY, bool WIRE, bool HB = false>
 __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0, uint32_t t1, uint8_t* rows0,
                                                   uint8_t* rows1, uint32_t* sums0, uint32_t* sums1, uint32_t lane,
                                                   Counters& cnt, u32x4* rec, uint32_t* verd, uint32_t* alo,
@@ -875,12 +894,12 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
     __builtin_amdgcn_wave_barrier();
     bool wb = WIRE ? wire_header_phase64(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, F0.ok, in0, F0.wend, cnt,
                                          &rec[0], &verd[0])
-                   : header_phase_ref(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, in0, F0.ok, F0.parse, cnt,
+                   : header_phase_ref<HB>(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, in0, F0.ok, F0.parse, cnt,
                                       &rec[0], &verd[0]);
     wbm[0] = __ballot(wb);
     wb = WIRE ? wire_header_phase64(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, F1.ok, in1, F1.wend, cnt, &rec[1],
                                     &verd[1])
-              : header_phase_ref(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, in1, F1.ok, F1.parse, cnt, &rec[1],
+              : header_phase_ref<HB>(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, in1, F1.ok, F1.parse, cnt, &rec[1],
                                  &verd[1]);
     wbm[1] = __ballot(wb);
     alo[0] = d0.x;
@@ -922,7 +941,7 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
 // ragged tiles (c4) the ranked step-packed streams.
 // ================================================================================================
 template <int TPW, int SYNC, bool WIRE, bool SUBT, bool TRACE, bool DLDS, bool WT, int HEAVY, int UR = kU,
-          bool USPLIT = false, bool PRIO = false, int SLACK = 0>
+          bool USPLIT = false, bool PRIO = false, int SLACK = 0, bool HB = false>
 __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, uint32_t t_end, Echo6Smem<TPW>& sm) {
     static_assert(SYNC == 0 || SYNC == 2, "write phases: at once (0) or heavy waves wait for the round (2)");
     static_assert(SLACK >= 0 && SLACK < kWaves6, "SLACK: waves a heavy wave does not wait for");
@@ -952,7 +971,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
         // ================= read phase =================
         bool paired = false;
         if (PAIR && r0 + wave < t_end && r0 + (uint32_t)kWaves6 + wave < t_end)  // wave-uniform
-            paired = read_round_short2<HEAVY, WIRE>(a, r0 + wave, r0 + (uint32_t)kWaves6 + wave, s_hdr[wave][0],
+            paired = read_round_short2<HEAVY, WIRE, HB>(a, r0 + wave, r0 + (uint32_t)kWaves6 + wave, s_hdr[wave][0],
                                               s_hdr[wave][TPW > 1 ? 1 : 0], sm.sum[wave][0], sm.sum[wave][1], lane,
                                               cnt, rec, verd, alo, ahi, wbm, round_long);
 #pragma unroll
@@ -1122,7 +1141,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                     wb = wire_header_phase64(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
                                              &verd_o);
                 else
-                    wb = header_phase_ref(a, rows + lane * kWin, ic_raw, addr, len, in_n, ok, parse, cnt, &rec_o,
+                    wb = header_phase_ref<HB>(a, rows + lane * kWin, ic_raw, addr, len, in_n, ok, parse, cnt, &rec_o,
                                           &verd_o);
                 wbm_o = __ballot(wb);
             } while (0);
@@ -1201,7 +1220,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // windows (44 / 280 / 185 us for c2 / c3 / c4 against 71 / 298 / 215 on the 128-B windows of rounds 1-4, in-process
 // A/B, profiles/r04/wire64/).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = SUBT ? 0 : kRefSlack>
+          int SLACK = SUBT ? 0 : kRefSlack, bool HB = false>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = SUBT ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW> sm;
@@ -1209,8 +1228,8 @@ __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, ui
     const uint32_t ntiles = (a.n + tl - 1) / tl;
     const uint32_t t_begin = blockIdx.x * tiles_per_wg;
     const uint32_t t_end = min(ntiles, t_begin + tiles_per_wg);
-    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, kRefHeavy, UR, USPLIT, PRIO, SLACK>(a, t_begin, t_end,
-                                                                                                    sm);
+    echo6_body<TPW, SUBT ? 0 : 2, WIRE, SUBT, false, false, !SUBT, kRefHeavy, UR, USPLIT, PRIO, SLACK, HB>(a, t_begin,
+                                                                                                        t_end, sm);
 }
 
 // Round kernel geometry: one workgroup per CU (fewer for small batches), equal contiguous tile shares.
