@@ -31,9 +31,9 @@ import torch  # noqa: E402
 METRIC = "Mframes/s + GiB/s device-resident, 1500B ICMP echo batch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # the transform kernel xsk_gpu_echo_dev launches for a large batch (the name rocprofv3 reports)
-KERNEL = "echo_round_kernel<false, false, 6, true, true, 2, false>"
+KERNEL = "echo_round_kernel<false, false, 6, true, true, 2, true>"
 # xsk_gpu_echo_dev_opts, nonzero --opts
-WIRE_KERNEL = "echo_round_kernel<true, false, 6, true, true, 2, false>"
+WIRE_KERNEL = "echo_round_kernel<true, false, 6, true, true, 2, true>"
 CONFIGS = {
     # name: (frames per GPU, len_lo, len_hi, stride, seed, description)
     "c2": (1 << 20, 64, 64, 64, 0x5EED0002, "c2: 1M x 64B minimum-size ICMP echo frames, packed 64-B stride"),

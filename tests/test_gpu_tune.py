@@ -17,8 +17,8 @@ import xsknet_amd as X  # noqa: E402
 # (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4, 22 / 23 wire as shipped with VLAN only /
 # SLACK 0, 42 HB (the header phase's window read with b128 LDS reads).  (Round 5 removed 14-18, 21 and 24 with their switches from the product header: RS 2, LASTW, the 128-B wire
 # windows and unpaired wire tiles, each lost in a committed A/B log.)
-VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 22, 23, 42]
-WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL}
+VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 22, 23, 42, 43]
+WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL, 43: X.OPT_ALL}
 # the short-tile grids of round 5 (tune/xsk_tune_product.hip SG / SGP, c2 experiments): they handle all-short batches
 # only, so they are checked on one (every tile pair short), every byte against the oracle
 SHORT_VARIANTS = [30, 32, 33, 35, 36, 37, 38, 39]
@@ -88,7 +88,7 @@ def test_product_switch_uniform_tiles(variant, flen):
             d_umem.copy_(to_dev(umem))
 
 
-@pytest.mark.parametrize("variant", [2, 22, 23])
+@pytest.mark.parametrize("variant", [2, 22, 23, 43])
 def test_product_wire_variants_on_wire_traffic(variant):
     """The wire-mode variants on the wire generator's traffic (tests/wire_frames.py: VLAN stacks, IHL 3-15 with
     options -- headers reaching past a 64-B window --, fragments, tot_len errors, padding, bad checksums,

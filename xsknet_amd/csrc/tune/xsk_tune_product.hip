@@ -61,12 +61,12 @@ __global__ __launch_bounds__(kThreads6, 1) void timed_round_kernel(EchoArgs a, u
         for (uint32_t k = 0;; ++k) {
             const uint32_t tb = (k * gridDim.x + blockIdx.x) * kRound;
             if (tb >= ntiles) break;
-            echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack>(a, tb, min(ntiles, tb + kRound), sm);
+            echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack, true>(a, tb, min(ntiles, tb + kRound), sm);
         }
     } else {
         const uint32_t g = (PERM == 1 && (blockIdx.x ^ 1u) < gridDim.x) ? blockIdx.x ^ 1u : blockIdx.x;
         const uint32_t t_begin = g * per, t_end = min(ntiles, t_begin + per);
-        echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack>(a, t_begin, t_end, sm);
+        echo6_body<kRefTPW, 2, false, false, false, false, true, kRefHeavy, kUR, true, true, kRefSlack, true>(a, t_begin, t_end, sm);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -470,9 +470,10 @@ extern "C" int xsk_gpu__product_variant(int variant, uint32_t grid_force, void* 
         // 40 / 41: diagnostics (wrong outputs): SG without the header phase / without LDS and header phase
         case 40: if (short_grid<false, 4, true, 1>(args, s)) return -EINVAL; break;
         case 41: if (short_grid<false, 4, true, 2>(args, s)) return -EINVAL; break;
-        // 42: HB -- the reference header phase's window read as three ds_read_b128 (aligned waves) and an aligned
-        // reply's patch stored as two b128 + one b64
-        case 42: echo_round_kernel<false, false, kUR, true, true, kRefSlack, true><<<gg, bb, 0, s>>>(args, per); break;
+        // 42 / 43: without HB (shipped in round 5: the header phase's window read as three ds_read_b128 in aligned waves,
+        // an aligned reply's patch stored as two b128 + one b64) -- eleven ds_read_b32, seven ds_write_b32; reference / wire
+        case 42: echo_round_kernel<false, false, kUR, true, true, kRefSlack, false><<<gg, bb, 0, s>>>(args, per); break;
+        case 43: args.opts = XSK_GPU_OPT_ALL; echo_round_kernel<true, false, kUR, true, true, kRefSlack, false><<<gg, bb, 0, s>>>(args, per); break;
         // timing probes: workgroup stamps at workspace u64 offset 8192 (grid <= 1024: 4096 u64)
         case 10: timed_round_kernel<0><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;
         case 11: timed_round_kernel<1><<<gg, bb, 0, s>>>(args, per, args.partials + 8192); break;

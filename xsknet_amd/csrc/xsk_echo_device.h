@@ -445,10 +445,13 @@ __device__ __forceinline__ void stream_tile_uniform(__amdgpu_buffer_rsrc_t rsrc,
 // patched in LDS and returns true (the caller stores the whole window), any other reply is written here,
 // byte-exact.
 // ================================================================================================
-// HB (tuning switch, round 5): a wave whose frames all start 16-B aligned reads its window's first 48 bytes with three
+// HB (round 5, shipped): a wave whose frames all start 16-B aligned reads its window's first 48 bytes with three
 // ds_read_b128 instead of eleven ds_read_b32 -- the rows are 64 B apart, so a b32 read of one dword in every row meets
 // 16 lanes on each of two banks (16-way), a b128 read 4-way -- and an aligned reply's patch goes back as two b128 and one
-// b64 store instead of seven b32 ones (the unchanged dwords 3-5 rewritten with the values read).
+// b64 store instead of seven b32 ones (the unchanged dwords 3-5 rewritten with the values read).  c2 LDS bank-conflict
+// cycles 6.72 M -> 1.87 M per launch; in-process A/B over two sessions, µs: c2 34.94 / 35.00 -> 34.20 / 34.36, c3 274.3 /
+// 274.7 -> 272.8 / 273.3, c4 179.6 / 180.3 -> 178.5 / 179.2, p98 63.8 / 63.9 -> 62.6 / 62.7; wire mode (every option)
+// c2 36.5 -> 35.0, c3 275.2 -> 274.5, c4 183.0 -> 182.1 (profiles/r05/hb/).
 template <bool HB = false>
 __device__ __forceinline__ bool header_phase_ref(const EchoArgs& a, uint8_t* row, uint32_t ic_raw, uint64_t addr,
                                                  uint32_t len, bool live, bool ok, bool parse, Counters& cnt,
@@ -602,6 +605,7 @@ __device__ __forceinline__ uint64_t sum_row_range(const uint8_t* rb, uint32_t lo
     return acc;
 }
 
+template <bool HB = false>
 __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* row, uint32_t ic_raw, uint64_t addr,
                                                     uint32_t len, bool ok, bool live, uint32_t wend, Counters& cnt,
                                                     u32x4* rec_out, uint32_t* verd_out) {
@@ -616,10 +620,16 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
     auto be16 = [&](uint32_t i) -> uint32_t { return (fb(i) << 8) | fb(i + 1); };
     // the frame's first 40 bytes as frame-relative LE dwords (window bytes off .. off + 43 < 64): an untagged frame's
     // fields at constant offsets come from registers instead of one LDS byte read each
-    const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
     uint32_t h[10];
+    if (HB && __ballot(off != 0u) == 0ull) {  // as header_phase_ref<HB>: three ds_read_b128 for an aligned wave
+        const u32x4 q0 = *(const u32x4*)row, q1 = *(const u32x4*)(row + 16), q2 = *(const u32x4*)(row + 32);
+        h[0] = q0.x, h[1] = q0.y, h[2] = q0.z, h[3] = q0.w, h[4] = q1.x, h[5] = q1.y, h[6] = q1.z, h[7] = q1.w;
+        h[8] = q2.x, h[9] = q2.y;
+    } else {
+        const uint32_t* rw = (const uint32_t*)(row + (off & ~3u));
 #pragma unroll
-    for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+        for (int k = 0; k < 10; ++k) h[k] = __builtin_amdgcn_alignbyte(rw[k + 1], rw[k], off & 3u);
+    }
     auto hb = [&](uint32_t i) -> uint32_t { return (h[i >> 2] >> (8u * (i & 3u))) & 0xFFu; };  // i < 40, constant
     auto hbe16 = [&](uint32_t i) -> uint32_t { return (hb(i) << 8) | hb(i + 1u); };
     uint32_t verdict = XSK_GPU_TX_REPLY;
@@ -724,13 +734,20 @@ __device__ __forceinline__ bool wire_header_phase64(const EchoArgs& a, uint8_t* 
             const uint32_t n8 = (h[7] & 0xFFFFu) | (h[8] & 0xFF000000u);  // saddr[2:4] | type=0 | code
             if (off == 0u && wend >= (uint32_t)kWin) {
                 uint32_t* r32 = (uint32_t*)row;  // patched in LDS, stored as a whole window in the write phase
-                r32[0] = n0;
-                r32[1] = n1;
-                r32[2] = n2;
-                r32[6] = n6;
-                r32[7] = n7;
-                r32[8] = n8;
-                r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+                if (HB) {
+                    *(u32x4*)row = u32x4{n0, n1, n2, h[3]};
+                    *(u32x4*)(row + 16) = u32x4{h[4], h[5], n6, n7};
+                    r32[8] = n8;
+                    r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+                } else {
+                    r32[0] = n0;
+                    r32[1] = n1;
+                    r32[2] = n2;
+                    r32[6] = n6;
+                    r32[7] = n7;
+                    r32[8] = n8;
+                    r32[9] = (h[9] & 0xFFFF0000u) | csum_new_le;
+                }
                 wb = true;
             } else {  // byte-exact: only the rewritten bytes
                 uint8_t* pkt = a.umem + addr;
@@ -892,12 +909,12 @@ __device__ __forceinline__ bool read_round_short2(const EchoArgs& a, uint32_t t0
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    bool wb = WIRE ? wire_header_phase64(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, F0.ok, in0, F0.wend, cnt,
+    bool wb = WIRE ? wire_header_phase64<HB>(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, F0.ok, in0, F0.wend, cnt,
                                          &rec[0], &verd[0])
                    : header_phase_ref<HB>(a, rows0 + lane * kWin, sums0[lane], F0.addr, F0.len, in0, F0.ok, F0.parse, cnt,
                                       &rec[0], &verd[0]);
     wbm[0] = __ballot(wb);
-    wb = WIRE ? wire_header_phase64(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, F1.ok, in1, F1.wend, cnt, &rec[1],
+    wb = WIRE ? wire_header_phase64<HB>(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, F1.ok, in1, F1.wend, cnt, &rec[1],
                                     &verd[1])
               : header_phase_ref<HB>(a, rows1 + lane * kWin, sums1[lane], F1.addr, F1.len, in1, F1.ok, F1.parse, cnt, &rec[1],
                                  &verd[1]);
@@ -1138,7 +1155,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
                 const uint32_t ic_raw = nit ? sums_ic[lane] : 0u;
                 bool wb;
                 if (WIRE)
-                    wb = wire_header_phase64(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
+                    wb = wire_header_phase64<HB>(a, rows + lane * kRowW, ic_raw, addr, len, ok, in_n, wend, cnt, &rec_o,
                                              &verd_o);
                 else
                     wb = header_phase_ref<HB>(a, rows + lane * kWin, ic_raw, addr, len, in_n, ok, parse, cnt, &rec_o,
@@ -1220,7 +1237,7 @@ __device__ __forceinline__ void echo6_body(const EchoArgs& a, uint32_t t_begin, 
 // windows (44 / 280 / 185 us for c2 / c3 / c4 against 71 / 298 / 215 on the 128-B windows of rounds 1-4, in-process
 // A/B, profiles/r04/wire64/).
 template <bool WIRE, bool SUBT, int UR = SUBT ? kU : kUR, bool USPLIT = !SUBT, bool PRIO = !SUBT,
-          int SLACK = SUBT ? 0 : kRefSlack, bool HB = false>
+          int SLACK = SUBT ? 0 : kRefSlack, bool HB = true>
 __global__ __launch_bounds__(kThreads6, 1) void echo_round_kernel(EchoArgs a, uint32_t tiles_per_wg) {
     constexpr int TPW = SUBT ? 1 : kRefTPW;
     __shared__ Echo6Smem<TPW> sm;

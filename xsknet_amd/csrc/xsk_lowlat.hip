@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
         if (ntiles)
             // wire mode on the reference form's 64-B windows and streams with wire_header_phase64 (the 128-B form took
             // 11.6 us per 64 x 64-B call with every option against 8.7 in reference mode, profiles/r04/wll/)
-            echo6_body<kLLTPW, kLLSync, WIRE, true, true, true, false, kRefHeavy, kU, false, false, 0>(a, 0u,
+            echo6_body<kLLTPW, kLLSync, WIRE, true, true, true, false, kRefHeavy, kU, false, false, 0, true>(a, 0u,
                                                                                                           ntiles, sm);
         // the two polls' registers live across the body: a batch is taken while the other poll is still in
         // flight, and registers the compiler reused would first have to wait for it to land
