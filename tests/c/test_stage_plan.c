@@ -118,6 +118,36 @@ int main(void) {
     }
     p = xsk_gpu__stage_plan(d, 10, U, 0, 1, 1);
     assert(p.kind == XSK_STAGE_NONE && p.contained && p.sum == 0 && !p.aligned);
+    /* 7. the host pack's partition into staging halves: every frame in exactly one half, each half within its bytes,
+     *    at least one frame per half, frames too large for a half carried without bytes */
+    {
+        uint64_t seed = 12345;
+        for (int t = 0; t < 200; t++) {
+            const uint32_t n = 1u + (uint32_t)(seed % 3000u);
+            const uint64_t half = 4096u << (seed % 8u);
+            for (uint32_t i = 0; i < n; i++) {
+                seed = seed * 6364136223846793005ull + 1442695040888963407ull;
+                d[i].addr = (seed >> 20) % (1u << 29);
+                d[i].len = (uint32_t)((seed >> 40) % (t % 3 == 0 ? 70000u : 1600u));
+            }
+            uint32_t f0 = 0, halves = 0;
+            while (f0 < n) {
+                uint64_t bytes = 0;
+                const uint32_t f1 = xsk_gpu__hostpack_split(d, f0, n, U, t & 1, half, &bytes);
+                assert(f1 > f0 && f1 <= n);
+                uint64_t want = 0;
+                for (uint32_t f = f0; f < f1; f++) {
+                    uint64_t a16 = 0;
+                    const uint64_t sp = xsk_gpu__read_span(d[f].addr, d[f].len, U, t & 1, &a16);
+                    want += sp + 16u > half ? 0u : sp;
+                }
+                assert(bytes == want && ((((uint64_t)(f1 - f0) * 4u + 15u) & ~15ull) + bytes <= half));
+                f0 = f1;
+                halves++;
+            }
+            assert(halves >= 1);
+        }
+    }
     printf("stage plan ok\n");
     return 0;
 }

@@ -368,16 +368,8 @@ static int stage_hostpack(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const st
             if (hipEventCreateWithFlags(&c->stage_ev[h], hipEventDisableTiming) != hipSuccess) return -EIO;
     }
     for (uint32_t f0 = 0; f0 < n;) {
-        /* the frames [f0, f1) whose offsets table and spans fit one half (a frame too large for any half: 0 bytes) */
-        uint32_t f1 = f0;
-        uint64_t bytes = 0;
-        for (; f1 < n; f1++) {
-            uint64_t a16 = 0;
-            const uint64_t sp = xsk_gpu__read_span(d[f1].addr, d[f1].len, c->umem_size, wire, &a16);
-            const uint64_t b = sp + 16u > half ? 0u : sp;
-            if ((((uint64_t)(f1 - f0 + 1) * 4u + 15u) & ~15ull) + bytes + b > half) break;
-            bytes += b;
-        }
+        uint64_t bytes = 0; /* the frames [f0, f1) whose offsets table and spans fit one half */
+        const uint32_t f1 = xsk_gpu__hostpack_split(d, f0, n, c->umem_size, wire, half, &bytes);
         const int h = c->stage_half;
         if (c->stage_rec[h] && hipEventSynchronize(c->stage_ev[h]) != hipSuccess) return -EIO;
         uint8_t* hs = c->h_stage + (size_t)h * half;

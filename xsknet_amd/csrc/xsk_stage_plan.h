@@ -49,7 +49,7 @@ static inline uint64_t xsk_gpu__uniform_stride(const struct xsk_gpu_desc* d, uin
     return s;
 }
 
-/* Plan chunk d[0..n) of a call.  wire: wire mode (128-B header windows); have_alias: the UMEM has a mapped device
+/* Plan chunk d[0..n) of a call.  wire: wire mode (frames parsed from 14 bytes on; the same 64-B windows); have_alias: the UMEM has a mapped device
  * alias on the context's device (the gather kernel's source); prefix_aligned: every frame of the call's EARLIER chunks
  * starts 16-B aligned.  The copy-in paths:
  *   - n <= XSK_GPU_LOWLAT_MAX (an RX-loop batch) with an alias: the gather kernel, whatever the layout (one launch beats a
@@ -103,6 +103,25 @@ static inline struct xsk_stage_plan xsk_gpu__stage_plan(const struct xsk_gpu_des
         p.contained = prefix && spans_own;
     }
     return p;
+}
+
+/* XSK_STAGE_HOSTPACK's partition of a chunk into staging halves: the frames [f0, return value) whose u32 offsets table
+ * (rounded up to 16 B) and read spans fit one half of `half` bytes.  A frame whose span cannot fit any half
+ * (span + 16 > half) is counted with no bytes -- it takes a DMA copy of its own -- so a half always takes at least one
+ * frame when f0 < n.  *bytes = the spans the half carries. */
+static inline uint32_t xsk_gpu__hostpack_split(const struct xsk_gpu_desc* d, uint32_t f0, uint32_t n, uint64_t umem_size,
+                                               int wire, uint64_t half, uint64_t* bytes) {
+    uint32_t f1 = f0;
+    uint64_t b = 0;
+    for (; f1 < n; f1++) {
+        uint64_t a16 = 0;
+        const uint64_t sp = xsk_gpu__read_span(d[f1].addr, d[f1].len, umem_size, wire, &a16);
+        const uint64_t x = sp + 16u > half ? 0u : sp;
+        if ((((uint64_t)(f1 - f0 + 1) * 4u + 15u) & ~15ull) + b + x > half) break;
+        b += x;
+    }
+    *bytes = b;
+    return f1;
 }
 
 #ifdef __cplusplus
