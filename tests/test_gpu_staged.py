@@ -366,6 +366,60 @@ def test_staged_no_alias_multi_chunk_and_jumbo():
     assert rec["hostpack"] == 1 and rec["own_dma"] == int(big.sum()), rec
 
 
+def test_staged_no_alias_unaligned_wire_and_umem_end():
+    """The host pack on the layouts that stress it: (a) packed odd-length frames, descriptors interleaved over three
+    chunks -- unaligned frames whose read spans overlap their neighbours' (every chunk ordered behind the previous pack);
+    (b) wire mode with every option over scrambled mixed traffic; (c) frames ending at the last bytes of the UMEM, whose
+    64-B window is cut by the UMEM's end, at every start offset.  Without an alias, and with it for (c): exact."""
+    _dev()
+    # (a)
+    n = 2 * CHUNK + 333
+    lens = np.random.default_rng(78).integers(1537, 1552, n).astype(np.uint32)
+    umem, descs = packed(lens, 0x5EED6363)
+    descs = np.ascontiguousarray(descs[np.concatenate([np.arange(c, n, 3) for c in range(3)])])
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
+        ctx.drop_alias(1 << 20)
+        v, r, st = ctx.process(descs)
+        rec = ctx.staged_stats()
+    check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
+    assert rec["contained"] == 0 and rec["hostpack"] + rec["span"] == len(stage_chunks(n)), rec
+    # (b)
+    n = CHUNK + 2345
+    umem, descs = scrambled(n, n + 999, 2048, 0, 0x5EED6464, mode=1, lo=14, hi=1500)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
+    for batch in (n, 64):
+        work = umem.copy()
+        with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_STAGED, opts=X.OPT_ALL) as ctx:
+            ctx.drop_alias()
+            v, r, tot = run_batches(ctx, descs, batch)
+            rec = ctx.staged_stats()
+        assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all(), batch
+        for k in COUNTERS:
+            assert tot[k] == int(s_ref[k]), (batch, k)
+        assert rec["hostpack"] > 0 and rec["gather"] == 0, (batch, rec)
+    # (c) one frame per call, ending at the UMEM's last byte, start offsets 0..15 (len 42..57)
+    for alias in (True, False):
+        for off in range(16):
+            size = 8192
+            umem = np.zeros(size, np.uint8)
+            length = 42 + off
+            tmp = np.zeros(4096, np.uint8)
+            d0 = oracle.synth_batch(tmp, 1, 0, 4096, seed=0x5EED6565 + off, mode=0, len_lo=length, len_hi=length)
+            a = size - length
+            umem[a:] = tmp[:length]
+            descs = np.zeros(1, X.DESC_DTYPE)
+            descs[0] = (a, length, 0)
+            work = umem.copy()
+            with X.EchoContext(work, 0, max_batch=4096, mode=X.MODE_STAGED) as ctx:
+                if not alias:
+                    ctx.drop_alias()
+                v, r, st = ctx.process(descs)
+            check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
+            assert int(v[0]) == X.TX_REPLY and d0["len"][0] == length
+
+
 def test_staged_no_alias_multi_context():
     """xsk_gpu_multi G = 2 (both on the one GPU) whose contexts have no alias: each context's share takes the host
     pack, exact, and the per-context records (xsk_gpu__multi_ctx) add up to the frames' spans plus offsets."""

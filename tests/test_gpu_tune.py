@@ -19,10 +19,6 @@ import xsknet_amd as X  # noqa: E402
 # windows and unpaired wire tiles, each lost in a committed A/B log.)
 VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 22, 23, 42, 43]
 WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL, 43: X.OPT_ALL}
-# the short-tile grids of round 5 (tune/xsk_tune_product.hip SG / SGP, c2 experiments): they handle all-short batches
-# only, so they are checked on one (every tile pair short), every byte against the oracle
-SHORT_VARIANTS = [30, 32, 33, 35, 36, 37, 38, 39]
-WIRE_OPTS.update({35: X.OPT_ALL})
 
 
 @pytest.mark.parametrize("variant,grid", [(v, 0) for v in VARIANTS] + [(2, 3)])
@@ -136,36 +132,4 @@ def test_product_wire_variants_on_wire_traffic(variant):
     diff = np.nonzero(out != ref)[0]
     assert len(diff) == 0, f"{len(diff)} bytes differ, first at {diff[:8]}"
     part = ws[:1 << 15].cpu().numpy().view(np.uint64).reshape(-1, 4).sum(axis=0)
-    assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
-
-
-@pytest.mark.parametrize("variant", SHORT_VARIANTS)
-@pytest.mark.parametrize("stride,off", [(64, 0), (80, 8)])
-def test_short_tile_grid_variants(variant, stride, off):
-    """The c2 experiments of round 5 (SG: short-tile pairs on a non-persistent grid; SGP: the same with a software
-    pipeline over each wave's pairs) on an all-short batch of mixed traffic (every frame within its 64-B window: lengths
-    0-64 at a 64-B stride, or up to 56 at offset 8 of an 80-B stride): every byte, verdict, record and counter exact."""
-    dev = _dev()
-    L = X.tune_lib()
-    n = 128 * 70
-    umem = np.zeros(n * stride + 4096, np.uint8)
-    descs = oracle.synth_batch(umem, n, off, stride, seed=0x5EED6262 + variant, mode=1, len_lo=20,
-                               len_hi=64 - off)
-    assert int((descs["addr"] % 16 + descs["len"]).max()) <= 64
-    ref = umem.copy()
-    opts = WIRE_OPTS.get(variant, 0)
-    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
-    d_umem, d_descs = to_dev(umem), to_dev(descs)
-    d_verd = torch.zeros(n, dtype=torch.uint8, device=dev)
-    d_recs = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-    ws = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
-    rc = L.xsk_gpu__product_variant(variant, 0, d_umem.data_ptr(), d_umem.numel(), d_descs.data_ptr(), n,
-                                    d_verd.data_ptr(), d_recs.data_ptr(), ws.data_ptr(),
-                                    torch.cuda.current_stream().cuda_stream)
-    assert rc == 0
-    torch.cuda.synchronize()
-    assert (d_verd.cpu().numpy() == v_ref).all()
-    assert (d_recs.cpu().numpy().view(X.REC_DTYPE) == r_ref).all()
-    assert (d_umem.cpu().numpy() == ref).all()
-    part = ws.cpu().numpy().view(np.uint64).reshape(-1, 4).sum(axis=0)
     assert [int(x) for x in part] == [int(s_ref[k]) for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")]
