@@ -13,10 +13,11 @@ pytestmark = pytest.mark.gpu
 
 import xsknet_amd as X  # noqa: E402
 
-# 0 as shipped (reference), 2 wire mode as shipped, 5 / 6 no SPLIT
-# (reference / wire), 7 / 8 no PRIO (reference / wire), 9 / 13 SLACK 0 / 4, 22 / 23 wire as shipped with VLAN only /
-# SLACK 0, 42 HB (the header phase's window read with b128 LDS reads).  (Round 5 removed 14-18, 21 and 24 with their switches from the product header: RS 2, LASTW, the 128-B wire
-# windows and unpaired wire tiles, each lost in a committed A/B log.)
+# 0 as shipped (reference), 2 wire mode as shipped, 5 / 6 no SPLIT (reference / wire), 7 / 8 no PRIO (reference / wire),
+# 9 / 13 SLACK 0 / 4, 22 / 23 wire as shipped with VLAN only / SLACK 0, 42 / 43 without HB (the header phases' windows
+# read with eleven ds_read_b32 instead of three ds_read_b128; reference / wire).  (Round 5 removed 14-18, 21 and 24 with
+# their switches from the product header: RS 2, LASTW, the 128-B wire windows and unpaired wire tiles, each lost in a
+# committed A/B log.)
 VARIANTS = [0, 2, 5, 6, 7, 8, 9, 13, 22, 23, 42, 43]
 WIRE_OPTS = {2: X.OPT_ALL, 6: X.OPT_ALL, 8: X.OPT_ALL, 22: X.OPT_VLAN, 23: X.OPT_ALL, 43: X.OPT_ALL}
 
