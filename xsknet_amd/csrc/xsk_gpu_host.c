@@ -61,7 +61,9 @@ struct xsk_gpu_ctx {
     uint8_t* h_pack;  /* STAGED: pinned host copy of d_pack */
     uint8_t* h_verd;  /* pinned (mapped) verdict staging */
     struct xsk_gpu_stats* h_stats; /* [max_chunks], pinned (mapped) */
-    struct xsk_gpu_desc* h_descs;  /* ZEROCOPY: pinned (mapped) descriptor staging */
+    struct xsk_gpu_desc* h_descs;  /* ZEROCOPY: pinned (mapped) descriptor staging; STAGED: pinned descriptor staging
+                                    * (the copy stream's descriptor copies are then true DMA copies, not the runtime's
+                                    * synchronous pageable path) */
     struct xsk_gpu_desc* m_descs;  /* ZEROCOPY: device aliases of h_descs / h_verd / h_stats */
     uint8_t* m_verd;
     struct xsk_gpu_stats* m_stats;
@@ -258,6 +260,7 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     }
     TRY(hipHostMalloc((void**)&c->h_verd, max_batch, hipHostMallocMapped));
     TRY(hipHostMalloc((void**)&c->h_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats), hipHostMallocMapped));
+    if (!zerocopy(c)) TRY(hipHostMalloc((void**)&c->h_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc), 0));
     if (zerocopy(c)) {
         TRY(hipHostMalloc((void**)&c->h_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc), hipHostMallocMapped));
         TRY(hipHostGetDevicePointer((void**)&c->m_descs, c->h_descs, 0));
@@ -467,7 +470,9 @@ static int enqueue_chunk(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint3
     (void)s;
     const hipStream_t sa = c->stream[0], sb = c->stream[1];
     struct xsk_gpu_desc* dd = c->d_descs + i0;
-    TRY(hipMemcpyAsync(dd, descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, sa));
+    /* (slot i0.. of the pinned staging is not reused within a call, and the previous call has drained) */
+    memcpy(c->h_descs + i0, descs + i0, (size_t)n * sizeof *descs);
+    TRY(hipMemcpyAsync(dd, c->h_descs + i0, (size_t)n * sizeof *descs, hipMemcpyHostToDevice, sa));
     const struct xsk_stage_plan p =
         xsk_gpu__stage_plan(descs + i0, n, c->umem_size, c->opts != 0, c->m_umem != NULL, *prefix_aligned);
     *prefix_aligned &= (int)p.aligned;
