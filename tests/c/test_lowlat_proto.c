@@ -212,7 +212,7 @@ int main(void) {
             assert(next == n);
         }
 
-    /* 10. groups: <= 64 frames on the leader; 1024 x 1500 B on every workgroup; 300 x 64 B on 2 */
+    /* 10. groups: <= 64 frames on the leader, and <= 128 frames of <= 16 KiB; every larger batch on every workgroup */
     struct xsk_gpu_desc d[XSK_GPU_LOWLAT_MAX];
     for (int i = 0; i < (int)XSK_GPU_LOWLAT_MAX; i++) {
         d[i].addr = 4096u * i;
@@ -220,11 +220,16 @@ int main(void) {
         d[i].options = 0;
     }
     assert(xsk_gpu__ll_groups(d, 64) == 1);
-    assert(xsk_gpu__ll_groups(d, 100) == 1); /* 146 KiB */
-    assert(xsk_gpu__ll_groups(d, 256) == 2); /* 375 KiB */
+    assert(xsk_gpu__ll_groups(d, 65) == XSK_GPU__LL_WG);  /* 95 KiB */
+    assert(xsk_gpu__ll_groups(d, 100) == XSK_GPU__LL_WG); /* 146 KiB */
     assert(xsk_gpu__ll_groups(d, XSK_GPU_LOWLAT_MAX) == XSK_GPU__LL_WG);
     for (int i = 0; i < (int)XSK_GPU_LOWLAT_MAX; i++) d[i].len = 64;
-    assert(xsk_gpu__ll_groups(d, 300) == 2 && xsk_gpu__ll_groups(d, 256) == 1);
+    assert(xsk_gpu__ll_groups(d, 128) == 1 && xsk_gpu__ll_groups(d, 129) == XSK_GPU__LL_WG);
+    assert(xsk_gpu__ll_groups(d, 300) == XSK_GPU__LL_WG && xsk_gpu__ll_groups(d, 256) == XSK_GPU__LL_WG);
+    d[0].len = 1500;
+    assert(xsk_gpu__ll_groups(d, 128) == 1);  /* 9.5 KiB */
+    for (int i = 0; i < 16; i++) d[i].len = 1500;
+    assert(xsk_gpu__ll_groups(d, 128) == XSK_GPU__LL_WG);  /* 30 KiB */
     printf("lowlat proto ok\n");
     return 0;
 }

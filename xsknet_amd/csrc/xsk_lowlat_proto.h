@@ -72,18 +72,21 @@ struct xsk_gpu__bell {
 #define XSK_GPU__BELL_WG(w) ((uint64_t)((w) & 0x7u) << 56)
 #define XSK_GPU__BELL_STOP (1ull << 63)
 
-/* Workgroups for a doorbell batch: one per 256 frames or per 256 KiB of frame bytes, 1..XSK_GPU__LL_WG (one
- * CU caps the PCIe reads of a batch at ~17 GB/s: its waves have only so many loads in flight).  A batch of
- * <= 64 frames always runs on the leader alone, whose poll already brought its descriptors. */
+/* Workgroups for a doorbell batch.  A batch of <= 64 frames runs on the leader alone, whose poll already brought its
+ * descriptors, and so does one of <= 128 frames and <= 16 KiB (minimum-size frames: a second workgroup's own doorbell
+ * line and barrier cost more than it streams).  Any larger batch runs on all XSK_GPU__LL_WG: one CU caps the PCIe reads
+ * of a batch (its waves have only so many loads in flight), and in round 5's sweep (tools/hostlat.py --groups 1-4,
+ * 64 / 512 / 1500-B frames x 64-1024 per batch, profiles/r05/lowlat_groups.jsonl) four workgroups were within 1 us of
+ * the best count everywhere above that line while round 4's rule (one per 256 frames or 256 KiB) lost up to 4 us there:
+ * 128 x 1500 B 20.5 -> 17.5 us, 256 x 512 B 19.2 -> 15.6, 256 x 64 B 12.1 -> 10.5. */
 static inline uint32_t xsk_gpu__ll_groups(const struct xsk_gpu_desc* d, uint32_t n) {
     if (n <= 64u) return 1u;
-    uint64_t bytes = 0;
-    for (uint32_t i = 0; i < n; i++) bytes += d[i].len < 4096u ? d[i].len : 4096u;
-    uint64_t w = (n + 255u) / 256u;
-    const uint64_t wb = (bytes + (256u << 10) - 1u) / (256u << 10);
-    if (wb > w) w = wb;
-    if (w > XSK_GPU__LL_WG) w = XSK_GPU__LL_WG;
-    return (uint32_t)(w < 1 ? 1 : w);
+    if (n <= 128u) {
+        uint64_t bytes = 0;
+        for (uint32_t i = 0; i < n; i++) bytes += d[i].len < 4096u ? d[i].len : 4096u;
+        if (bytes <= (16u << 10)) return 1u;
+    }
+    return XSK_GPU__LL_WG;
 }
 
 /* Frames of workgroup g's slice of an n-frame batch over w workgroups: contiguous, a multiple of 4 frames
