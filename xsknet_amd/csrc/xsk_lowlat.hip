@@ -7,7 +7,7 @@
 // (echo6_body, xsk_echo_device.h — the same code the launched kernel runs, bit for bit) over their slices of
 // the posted descriptors, write verdicts and records into mapped host memory, and publish completion (the
 // host adds the counters from the descriptors and verdicts it has anyway).  A batch of <= 64 frames (and any
-// batch under 256 frames and 256 KiB) is served by workgroup 0 alone; larger ones by up to XSK_GPU__LL_WG,
+// batch of <= 128 frames and <= 16 KiB) is served by workgroup 0 alone; larger ones by all XSK_GPU__LL_WG,
 // because one CU caps the PCIe reads of a batch (its waves have only so many loads in flight).
 // A batch is "write descriptors, bump the doorbell, spin on the completion words": no launch, no sync.
 // The host side of the protocol (posting, waiting, relaunch, timeout and recovery) is
