@@ -7,7 +7,8 @@ at any byte offset, in a shuffled descriptor order (the RX ring after AF_XDP's f
 `src/lib/xsk_receive.c:55-71`), plus a few descriptors that do not fit the UMEM.  The frames are the generator's
 reference-mode traffic (valid requests and every negative of SURVEY §8c) or the wire generator's (VLAN stacks, IHL
 3-15, fragments, padding, bad checksums).  Each case then runs through one entry point -- the device-resident call, a
-ZEROCOPY / STAGED (with or without the UMEM's device alias) / LOWLAT context in random batch splits -- with random wire
+ZEROCOPY / STAGED (with or without the UMEM's device alias) / LOWLAT context or a 2- or 3-context multi object on the one
+GPU in random batch splits -- with random wire
 options, and every byte of the UMEM, every verdict, record and counter must equal the oracle's.  Seeds are fixed: a
 failure names its case."""
 import numpy as np
@@ -22,7 +23,7 @@ import xsknet_amd as X  # noqa: E402
 from tests.test_gpu_host import COUNTERS  # noqa: E402
 from tests.wire_frames import random_frame  # noqa: E402
 
-ENTRIES = ["device", "zerocopy", "staged", "staged_noalias", "lowlat"]
+ENTRIES = ["device", "zerocopy", "staged", "staged_noalias", "lowlat", "multi"]
 OPTS = [0, 0, X.OPT_STRICT_IPV4, X.OPT_VLAN, X.OPT_VERIFY_CSUM, X.OPT_ALL]
 
 
@@ -107,13 +108,16 @@ def test_fuzz_parity(seed):
         st = d_stats.cpu().numpy().view(X.STATS_DTYPE)[0]
         tot = {k: int(st[k]) for k in COUNTERS}
     else:
+        rng = np.random.default_rng(seed)
         mode = {"zerocopy": X.MODE_ZEROCOPY, "staged": X.MODE_STAGED, "staged_noalias": X.MODE_STAGED,
-                "lowlat": X.MODE_LOWLAT}[entry]
+                "lowlat": X.MODE_LOWLAT, "multi": int(rng.choice([X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT]))}[entry]
         work = umem.copy()
         vs, rs, tot = [], [], {k: 0 for k in COUNTERS}
-        with X.EchoContext(work, 0, max_batch=splits, mode=mode, opts=opts) as ctx:
+        mk = (lambda: X.MultiContext(work, [0] * int(rng.integers(2, 4)), max_batch=splits, mode=mode, opts=opts)) \
+            if entry == "multi" else (lambda: X.EchoContext(work, 0, max_batch=splits, mode=mode, opts=opts))
+        with mk() as ctx:
             if entry == "staged_noalias":
-                ctx.drop_alias(int(np.random.default_rng(seed).choice([0, 8192, 65536])))
+                ctx.drop_alias(int(rng.choice([0, 8192, 65536])))
             for i in range(0, n, splits):
                 v, r, st = ctx.process(descs[i:i + splits])
                 vs.append(v)
