@@ -358,17 +358,27 @@ static int stage_hostpack(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const st
                           hipStream_t st) {
     const int wire = c->opts != 0;
     const uint64_t half = c->stage_bytes;
-    if (!c->h_stage) { /* first use */
-        if (hipHostMalloc((void**)&c->h_stage, 2u * (size_t)half, hipHostMallocDefault) != hipSuccess) {
-            c->h_stage = NULL;
-            return -ENOMEM;
+    if (!c->h_stage) { /* first use: all of it or nothing (a later call retries) */
+        uint8_t *hs = NULL, *ds = NULL;
+        hipEvent_t ev[2] = {NULL, NULL};
+        int rc = 0;
+        if (hipHostMalloc((void**)&hs, 2u * (size_t)half, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc((void**)&ds, 2u * (size_t)half) != hipSuccess)
+            rc = -ENOMEM;
+        for (int h = 0; h < 2 && !rc; h++)
+            if (hipEventCreateWithFlags(&ev[h], hipEventDisableTiming) != hipSuccess) rc = -EIO;
+        if (rc) {
+            if (hs) (void)hipHostFree(hs);
+            if (ds) (void)hipFree(ds);
+            for (int h = 0; h < 2; h++)
+                if (ev[h]) (void)hipEventDestroy(ev[h]);
+            return rc;
         }
-        if (hipMalloc((void**)&c->d_stage, 2u * (size_t)half) != hipSuccess) {
-            c->d_stage = NULL;
-            return -ENOMEM;
-        }
-        for (int h = 0; h < 2; h++)
-            if (hipEventCreateWithFlags(&c->stage_ev[h], hipEventDisableTiming) != hipSuccess) return -EIO;
+        c->h_stage = hs;
+        c->d_stage = ds;
+        c->stage_ev[0] = ev[0];
+        c->stage_ev[1] = ev[1];
+        c->stage_rec[0] = c->stage_rec[1] = 0;
     }
     for (uint32_t f0 = 0; f0 < n;) {
         uint64_t bytes = 0; /* the frames [f0, f1) whose offsets table and spans fit one half */
