@@ -382,6 +382,38 @@ int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ri
  * from the completion ring back to `pool`.  Returns the number moved. */
 uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_pool* pool, uint32_t max);
 
+/* Pipelined RX loop: xsk_gpu_rx_step with up to `depth` batches in flight, so that one queue's steps overlap their
+ * PCIe round trips instead of paying one per step.  The object owns `depth` contexts of `mode` over one registration
+ * of the UMEM (LOWLAT contexts beyond the device's resident-kernel slots run as ZEROCOPY, as xsk_gpu_init does) and
+ * hands batches to them in turn.  Frames of different batches are different frames, so batches in flight never
+ * share a byte (the ownership contract above).
+ *
+ * xsk_gpu_rx_pipe_step:
+ *   1. if a context is free and the RX ring holds descriptors: peek up to min(max_batch, XSK_GPU_RX_MAX_STEP) of them,
+ *      refill the fill ring (as xsk_gpu_rx_step), submit them and release the RX entries (the object keeps a copy of
+ *      the descriptors: res->received);
+ *   2. complete batches in submission order -- the oldest when every context is busy, any that are already done, and
+ *      all of them when step 1 found the RX ring empty -- each like xsk_gpu_rx_step's steps 4 and 5: replies onto the
+ *      TX ring (or dropped and freed when it is full), every other frame back to `pool`, counters.
+ * Returns the frames completed by this call (not the frames received), or a negative errno.  A batch whose completion
+ * fails stays the oldest in flight and the error is returned; the next step or flush runs it again through its
+ * context (as a caller retries a failed xsk_gpu_rx_step).  A failed submit leaves its frames on the RX ring.
+ * xsk_gpu_rx_pipe_flush completes every batch in flight (an idle link, teardown).  xsk_gpu_rx_pipe_fini waits for
+ * batches still in flight and drops their results: flush first.  Single caller thread, like a context. */
+#define XSK_GPU_RX_PIPE_MAX 4u
+typedef struct xsk_gpu_rx_pipe xsk_gpu_rx_pipe;
+int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t umem_size, uint32_t depth, int mode);
+int xsk_gpu_rx_pipe_step(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* rx, struct xsk_gpu_ring* fill, struct xsk_gpu_ring* tx,
+                         struct xsk_gpu_frame_pool* pool, uint32_t max_batch, struct xsk_gpu_stats* stats,
+                         struct xsk_gpu_rx_result* res);
+int xsk_gpu_rx_pipe_flush(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* tx, struct xsk_gpu_frame_pool* pool,
+                          struct xsk_gpu_stats* stats, struct xsk_gpu_rx_result* res);
+/* xsk_gpu_set_options on every context; -EBUSY while a batch is in flight. */
+int xsk_gpu_rx_pipe_set_options(xsk_gpu_rx_pipe* p, uint32_t opts);
+/* Batches in flight now. */
+uint32_t xsk_gpu_rx_pipe_inflight(const xsk_gpu_rx_pipe* p);
+void xsk_gpu_rx_pipe_fini(xsk_gpu_rx_pipe* p);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Bench / test utilities (not on the hot path).                                               */
 /* ------------------------------------------------------------------------------------------ */

@@ -4,8 +4,9 @@
  * Cases: normal service over 1..4 workgroups, the leader's idle exit and the Dekker relaunch, an instance that exits
  * without serving, the timeout with nothing served (an instance still queued when the call gave up -- ADVICE r03),
  * with part of the batch served, with the batch finished by an instance that was inside its body (a late
- * completion: 0), the broken channel (-EBUSY until the instance has stopped, then recovery), and in every case that
- * no relaunched grid ever serves a batch whose call has returned.  Built and run by tests/test_lowlat_proto.py. */
+ * completion: 0), the broken channel (-EBUSY until the instance has stopped, then recovery), the two halves of a call
+ * (begin / wait) on two channels with a batch in flight on each, and in every case that no relaunched grid ever
+ * serves a batch whose call has returned.  Built and run by tests/test_lowlat_proto.py. */
 #include <assert.h>
 #include <stdio.h>
 #include <string.h>
@@ -197,6 +198,59 @@ int main(void) {
     /* 8. stop: drains and clears */
     assert(xsk_gpu__ll_stop(&st, &o, -1.0) == 0 && !st.launched && S.running == 0);
     assert(xsk_gpu__ll_stop(&st, &o, -1.0) == 0); /* idempotent */
+
+    /* 8b. the two halves (the pipelined RX loop): two channels, a batch in flight on each, completed out of post order;
+     *     a second post while one is in flight is refused (nothing posted), ready never blocks, a wait with nothing in
+     *     flight is refused, and a stop while a batch is in flight ends it (its outcome in stop_unserved) */
+    {
+        struct sim A, B;
+        memset(&A, 0, sizeof A);
+        memset(&B, 0, sizeof B);
+        A.stop_countdown = B.stop_countdown = -1;
+        A.serve_mask = B.serve_mask = 0xFu;
+        A.serve_after = 3;
+        B.serve_after = 6;
+        A.stop_after = B.stop_after = 2;
+        struct xsk_gpu__ll_state sa = st, sb = st;
+        sa.bell = &A.bell;
+        sb.bell = &B.bell;
+        sa.seq = sb.seq = 0;
+        sa.launched = sb.launched = sa.broken = sb.broken = sa.inflight = sb.inflight = 0;
+        struct xsk_gpu__ll_ops oa = ops_of(&A), ob = ops_of(&B);
+        int want_a = 0, want_b = 0;
+        for (int round = 0; round < 20; round++) {
+            const uint32_t wa = 1u + (uint32_t)round % XSK_GPU__LL_WG, wb = 1u + (uint32_t)(round * 3) % XSK_GPU__LL_WG;
+            assert(xsk_gpu__ll_begin(&sa, &oa, XSK_GPU__BELL_N(64), wa) == 0 && sa.inflight);
+            assert(xsk_gpu__ll_begin(&sb, &ob, XSK_GPU__BELL_N(200), wb) == 0 && sb.inflight);
+            const uint64_t cmd = A.bell.cmd;
+            assert(xsk_gpu__ll_begin(&sa, &oa, XSK_GPU__BELL_N(64), wa) == -EBUSY && A.bell.cmd == cmd);
+            assert(!xsk_gpu__ll_ready(&sa) && !xsk_gpu__ll_ready(&sb)); /* nobody served anything yet */
+            if (round & 1) {
+                assert(xsk_gpu__ll_wait(&sb, &ob, &un) == 0 && un == 0 && !sb.inflight);
+                assert(xsk_gpu__ll_wait(&sa, &oa, &un) == 0 && un == 0);
+            } else {
+                for (int k = 0; k < 10; k++) oa.relax(oa.u); /* A's grid serves while the host does other work */
+                assert(xsk_gpu__ll_ready(&sa));
+                assert(xsk_gpu__ll_wait(&sa, &oa, &un) == 0 && un == 0);
+                assert(xsk_gpu__ll_wait(&sb, &ob, &un) == 0 && un == 0);
+            }
+            for (uint32_t g = 0; g < wa; g++) assert(A.bell.wg[g].done == sa.seq);
+            for (uint32_t g = 0; g < wb; g++) assert(B.bell.wg[g].done == sb.seq);
+            want_a += (int)wa;
+            want_b += (int)wb;
+        }
+        assert(A.serves == want_a && B.serves == want_b && A.launches == 1 && B.launches == 1); /* each slice once */
+        assert(xsk_gpu__ll_wait(&sa, &oa, &un) == -EINVAL);
+        /* stop with a batch in flight that nobody took: retired unserved, the state has nothing in flight */
+        A.serve_after = -1;
+        assert(xsk_gpu__ll_begin(&sa, &oa, XSK_GPU__BELL_N(64), 1) == 0);
+        assert(xsk_gpu__ll_stop(&sa, &oa, -1.0) == 0 && !sa.inflight && sa.stop_unserved == 1u);
+        assert(A.bell.wg[0].cancel == sa.seq && A.bell.wg[0].done == sa.seq);
+        assert(xsk_gpu__ll_wait(&sa, &oa, &un) == -EINVAL);
+        A.serve_after = 1;
+        assert(xsk_gpu__ll_run(&sa, &oa, XSK_GPU__BELL_N(64), 1, &un) == 0 && A.bell.wg[0].done == sa.seq);
+        assert(xsk_gpu__ll_stop(&sb, &ob, -1.0) == 0 && xsk_gpu__ll_stop(&sa, &oa, -1.0) == 0);
+    }
 
     /* 9. slices: contiguous, multiples of 4 (but the last), covering [0, n) exactly */
     for (uint32_t n = 1; n <= XSK_GPU_LOWLAT_MAX; n++)

@@ -12,6 +12,13 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+    if os.environ.get("XSK_TEST_NO_THP") == "1":  # diagnosis only: no transparent huge pages in this process
+        import ctypes
+        ctypes.CDLL(None).prctl(41, 1, 0, 0, 0)  # PR_SET_THP_DISABLE
+    if os.environ.get("XSK_TEST_NO_NUMA_BALANCING") == "1":  # diagnosis only: a task policy without MPOL_F_MOF
+        import ctypes
+        mask = ctypes.c_ulong(1)  # node 0
+        ctypes.CDLL(None, use_errno=True).syscall(238, 1, ctypes.byref(mask), 64)  # set_mempolicy(MPOL_PREFERRED)
 
 
 @pytest.fixture(scope="session", autouse=True)
@@ -33,3 +40,23 @@ def golden_kat():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "kat.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(autouse=True)
+def _no_resident_grid_outlives_its_channel(request):
+    """After every GPU test, once its contexts are collected, no LOWLAT resident grid may still run on cuda:0
+    (xsk_gpu__lowlat_live): a grid that outlived its channel would keep polling memory a later channel reuses."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return
+    except ImportError:
+        return
+    import gc
+    import xsknet_amd as X
+    gc.collect()
+    live = X.lowlat_live(0)
+    assert live == 0, f"{live} resident LOWLAT workgroups still running after {request.node.nodeid}"

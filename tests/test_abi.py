@@ -156,7 +156,8 @@ def test_tuning_code_is_not_in_the_product_library():
                                                     "xsk_gpu__echo_dev_grid", "xsk_gpu__multi_inject",
                                                     "xsk_gpu__staged_stats", "xsk_gpu__staged_noalias",
                                                     "xsk_gpu__multi_ctx", "xsk_gpu__lowlat_outcomes",
-                                                    "xsk_gpu__lowlat_test_width"}, \
+                                                    "xsk_gpu__lowlat_test_width", "xsk_gpu__rx_pipe_ctx",
+                                                    "xsk_gpu__lowlat_live"}, \
         exported - set(declared_functions())
     tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
                           check=True).stdout
@@ -184,7 +185,19 @@ def test_multi_and_lowlat_validation_without_gpu():
     assert L.xsk_gpu_multi_process(None, None, 0, None, None, None) == EINVAL
     assert L.xsk_gpu_multi_set_options(None, 1) == EINVAL
     L.xsk_gpu_multi_fini(None)
+    # the pipelined RX loop: depth 1..XSK_GPU_RX_PIPE_MAX, a valid mode, an aligned UMEM; NULL objects
+    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 0, 2) == EINVAL
+    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 5, 2) == EINVAL
+    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 2, 3) == EINVAL
+    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data + 1, 64, 2, 2) == EINVAL
+    assert L.xsk_gpu_rx_pipe_init(None, 0, buf.ctypes.data, 64, 2, 2) == EINVAL
+    assert L.xsk_gpu_rx_pipe_step(None, None, None, None, None, 64, None, None) == EINVAL
+    assert L.xsk_gpu_rx_pipe_flush(None, None, None, None, None) == EINVAL
+    assert L.xsk_gpu_rx_pipe_set_options(None, 0) == EINVAL
+    assert L.xsk_gpu_rx_pipe_inflight(None) == 0
+    L.xsk_gpu_rx_pipe_fini(None)
     hdr = open(HEADER).read()
+    assert "XSK_GPU_RX_PIPE_MAX 4u" in hdr
     assert "XSK_GPU_MODE_LOWLAT = 2" in hdr and f"XSK_GPU_LOWLAT_MAX {X.LOWLAT_MAX}u" in hdr
     assert f"XSK_GPU_MULTI_MAX {X.MULTI_MAX}" in hdr
 

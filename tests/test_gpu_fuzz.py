@@ -116,6 +116,9 @@ def test_fuzz_parity(seed):
         mk = (lambda: X.MultiContext(work, [0] * int(rng.integers(2, 4)), max_batch=splits, mode=mode, opts=opts)) \
             if entry == "multi" else (lambda: X.EchoContext(work, 0, max_batch=splits, mode=mode, opts=opts))
         with mk() as ctx:
+            modes = [X.ContextView(ctx.context(g)).mode for g in range(len(ctx.status()))] if entry == "multi" \
+                else [ctx.mode]
+            case += f" modes={modes}"
             if entry == "staged_noalias":
                 ctx.drop_alias(int(rng.choice([0, 8192, 65536])))
             for i in range(0, n, splits):
@@ -125,7 +128,11 @@ def test_fuzz_parity(seed):
                 for k in COUNTERS:
                     tot[k] += int(st[k])
         v, r = np.concatenate(vs), np.concatenate(rs)
-    assert (v == v_ref).all(), (case, np.nonzero(v != v_ref)[0][:8])
+    bad = np.nonzero(v != v_ref)[0]
+    if len(bad):
+        nb = np.nonzero(work != ref)[0]
+        raise AssertionError(f"{case}: {len(bad)} verdicts differ, first {bad[:8]}: got {v[bad[:8]]} want "
+                             f"{v_ref[bad[:8]]}, descs {descs[bad[:8]]}; {len(nb)} UMEM bytes differ, first {nb[:8]}")
     assert (r == r_ref).all(), (case, np.nonzero(r != r_ref)[0][:8])
     for k in COUNTERS:
         assert tot[k] == int(s_ref[k]), (case, k)

@@ -44,7 +44,22 @@ def check(umem, work, descs, v, r, tot):
     for k in COUNTERS:
         assert tot[k] == int(s_ref[k]), k
     diff = np.nonzero(work != ref)[0]
-    assert len(diff) == 0, f"{len(diff)} bytes differ, first at {diff[:8]}"
+    assert len(diff) == 0, f"{len(diff)} bytes differ, first at {diff[:8]}; " + describe_diff(umem, work, ref, descs, v,
+                                                                                               diff)
+
+
+def describe_diff(umem, work, ref, descs, v, diff):
+    """Which frames' bytes differ, where, and whether they are still the request's (a write that never landed)."""
+    addr = descs["addr"].astype(np.int64)
+    out = []
+    for j in np.unique(np.searchsorted(np.sort(addr), diff, side="right") - 1)[:6]:
+        a = int(np.sort(addr)[j])
+        i = int(np.nonzero(addr == a)[0][0])
+        d = diff[(diff >= a) & (diff < a + 4096)] - a
+        out.append(f"frame {i} @{a} len {int(descs['len'][i])} verdict {int(v[i])}: offsets {d[:24].tolist()} "
+                   f"got {work[a + d[:12]].tolist()} want {ref[a + d[:12]].tolist()} "
+                   f"request {umem[a + d[:12]].tolist()}")
+    return " | ".join(out)
 
 
 @pytest.mark.parametrize("mode", MODES)

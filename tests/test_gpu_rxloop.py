@@ -55,15 +55,10 @@ def _dev():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("mode,ctx_batch,step_batch", [(X.MODE_ZEROCOPY, 1024, 64), (X.MODE_STAGED, 1024, 64),
-                                                      (X.MODE_LOWLAT, 1024, 64), (X.MODE_LOWLAT, 64, 1024),
-                                                      (X.MODE_ZEROCOPY, 64, 1024), (X.MODE_STAGED, 1024, 1024)])
-def test_rx_loop_end_to_end(mode, ctx_batch, step_batch):
-    """ctx_batch < step_batch: the step peeks no more than the context takes (never an -EINVAL after the
-    fill ring was restocked).  The free stack recycles frames LIFO (xsk_receive.c:55-71), so after the first wrap
-    every step's addresses are scattered over the UMEM: STAGED steps of up to 1024 frames take the gather copy-in."""
-    _dev()
-    n_pkts, seed = 20000, 0x5EED0A0A
+def _drive(step, flush, step_batch, cap, n_pkts=20000, seed=0x5EED0A0A):
+    """Play the kernel side around `step(rx, fq, tx, pool, step_batch, totals) -> (frames completed, RxResult)` (and,
+    for a pipelined loop, `flush(tx, pool, totals)` once the last packet is in): every transmitted reply and every
+    frame handed back is checked byte for byte against the oracle, in RX order, and the counters at the end."""
     umem = np.zeros(NUM_FRAMES * FRAME_SIZE, np.uint8)
     rx, fq = KRing(X.DESC_DTYPE, False), KRing(np.uint64, True)
     tx, cq = KRing(X.DESC_DTYPE, True), KRing(np.uint64, False)
@@ -82,57 +77,143 @@ def test_rx_loop_end_to_end(mode, ctx_batch, step_batch):
     sent = 0
     replies_seen = 0
     delivered = collections.deque()  # RX order
-    with X.EchoContext(umem, 0, max_batch=ctx_batch, mode=mode) as ctx:
-        guard = 0
-        while sent < n_pkts or rx.k_avail():
-            guard += 1
-            assert guard < 100000
-            # kernel: deliver a burst into frames taken from the fill ring
-            burst = min(int(rng.integers(1, 200)), fq.k_avail(), RING - rx.k_avail(), n_pkts - sent)
-            descs = []
-            for addr in fq.k_pop(burst):
-                # aligned-chunk mode: the kernel masks a fill address to its chunk (the free stack
-                # holds descriptor addresses, headroom included, as xsk_free_umem_frame stores them)
-                a = (int(addr) & ~(FRAME_SIZE - 1)) + HEADROOM
-                L, buf = oracle.synth_frame(seed, sent, 1, 20, 1500, cap=FRAME_SIZE - HEADROOM)
-                umem[a:a + FRAME_SIZE - HEADROOM] = buf[:FRAME_SIZE - HEADROOM]
-                ref = buf[:FRAME_SIZE - HEADROOM].copy()
-                d1 = np.zeros(1, oracle.DESC_DTYPE)
-                d1[0] = (0, L, 0)
-                v, _, st = oracle.echo_batch(ref, d1)
-                for k in ref_tot:
-                    ref_tot[k] += int(st[k])
-                expect[a] = (sent, L, ref[:max(L, 64)].copy(), int(v[0]))
-                descs.append((a, L, 0))
-                delivered.append(a)
-                sent += 1
-            if descs:
-                rx.k_push(np.array(descs, X.DESC_DTYPE))
-            # app: one RX loop step (batches of 64 like RX_BATCH_SIZE), then completions
-            got, res = ctx.rx_step(rx.view, fq.view, tx.view, pool, step_batch, totals)
-            assert got <= min(ctx_batch, step_batch)
-            assert res.tx_full == 0
-            # kernel: transmit -> check bytes -> complete
-            txd = tx.k_pop(tx.k_avail())
-            for t in txd:
-                a, L = int(t["addr"]), int(t["len"])
+
+    def kernel_tx(got):
+        nonlocal replies_seen
+        # kernel: transmit -> check bytes -> complete
+        txd = tx.k_pop(tx.k_avail())
+        for t in txd:
+            a, L = int(t["addr"]), int(t["len"])
+            i, L0, exp, verdict = expect.pop(a)
+            assert L == L0 and verdict == X.TX_REPLY
+            assert bytes(umem[a:a + len(exp)]) == bytes(exp), i
+            replies_seen += 1
+        cq.k_push(np.array([int(t["addr"]) for t in txd], np.uint64))
+        X.lib().xsk_gpu_tx_complete(C.byref(cq.view), C.byref(pool), RING)
+        # frames the step completed but did not send went back to the pool untouched by anyone else yet: their bytes
+        # must match the oracle too
+        for _ in range(got):
+            a = delivered.popleft()
+            if a in expect:
                 i, L0, exp, verdict = expect.pop(a)
-                assert L == L0 and verdict == X.TX_REPLY
+                assert verdict != X.TX_REPLY
                 assert bytes(umem[a:a + len(exp)]) == bytes(exp), i
-                replies_seen += 1
-            cq.k_push(np.array([int(t["addr"]) for t in txd], np.uint64))
-            X.lib().xsk_gpu_tx_complete(C.byref(cq.view), C.byref(pool), RING)
-            # frames the step consumed but did not send went back to the pool untouched by anyone
-            # else yet: their bytes must match the oracle too
-            for _ in range(got):
-                a = delivered.popleft()
-                if a in expect:
-                    i, L0, exp, verdict = expect.pop(a)
-                    assert verdict != X.TX_REPLY
-                    assert bytes(umem[a:a + len(exp)]) == bytes(exp), i
-    assert sent == n_pkts
+
+    guard = 0
+    while sent < n_pkts or rx.k_avail():
+        guard += 1
+        assert guard < 100000
+        # kernel: deliver a burst into frames taken from the fill ring
+        burst = min(int(rng.integers(1, 200)), fq.k_avail(), RING - rx.k_avail(), n_pkts - sent)
+        descs = []
+        for addr in fq.k_pop(burst):
+            # aligned-chunk mode: the kernel masks a fill address to its chunk (the free stack
+            # holds descriptor addresses, headroom included, as xsk_free_umem_frame stores them)
+            a = (int(addr) & ~(FRAME_SIZE - 1)) + HEADROOM
+            L, buf = oracle.synth_frame(seed, sent, 1, 20, 1500, cap=FRAME_SIZE - HEADROOM)
+            umem[a:a + FRAME_SIZE - HEADROOM] = buf[:FRAME_SIZE - HEADROOM]
+            ref = buf[:FRAME_SIZE - HEADROOM].copy()
+            d1 = np.zeros(1, oracle.DESC_DTYPE)
+            d1[0] = (0, L, 0)
+            v, _, st = oracle.echo_batch(ref, d1)
+            for k in ref_tot:
+                ref_tot[k] += int(st[k])
+            expect[a] = (sent, L, ref[:max(L, 64)].copy(), int(v[0]))
+            descs.append((a, L, 0))
+            delivered.append(a)
+            sent += 1
+        if descs:
+            rx.k_push(np.array(descs, X.DESC_DTYPE))
+        got, res = step(umem, rx.view, fq.view, tx.view, pool, step_batch, totals)
+        assert got <= cap and res.received <= step_batch
+        assert res.tx_full == 0
+        kernel_tx(got)
+    if flush is not None:
+        got, res = flush(tx.view, pool, totals)
+        kernel_tx(got)
+    assert sent == n_pkts and not delivered and not expect
     assert replies_seen == ref_tot["tx_packets"]
     for k in ref_tot:
         assert int(totals[0][k]) == ref_tot[k], k
     # every frame is accounted for: free stack + fill ring + nothing in flight
     assert pool.n_free + fq.k_avail() == NUM_FRAMES
+    return umem
+
+
+@pytest.mark.parametrize("mode,ctx_batch,step_batch", [(X.MODE_ZEROCOPY, 1024, 64), (X.MODE_STAGED, 1024, 64),
+                                                      (X.MODE_LOWLAT, 1024, 64), (X.MODE_LOWLAT, 64, 1024),
+                                                      (X.MODE_ZEROCOPY, 64, 1024), (X.MODE_STAGED, 1024, 1024)])
+def test_rx_loop_end_to_end(mode, ctx_batch, step_batch):
+    """ctx_batch < step_batch: the step peeks no more than the context takes (never an -EINVAL after the
+    fill ring was restocked).  The free stack recycles frames LIFO (xsk_receive.c:55-71), so after the first wrap
+    every step's addresses are scattered over the UMEM: STAGED steps of up to 1024 frames take the gather copy-in."""
+    _dev()
+    holder = {}
+
+    def step(umem, rx, fq, tx, pool, n, totals):
+        if "ctx" not in holder:
+            holder["ctx"] = X.EchoContext(umem, 0, max_batch=ctx_batch, mode=mode)
+        return holder["ctx"].rx_step(rx, fq, tx, pool, n, totals)
+
+    try:
+        _drive(step, None, step_batch, min(ctx_batch, step_batch))
+    finally:
+        if "ctx" in holder:
+            holder["ctx"].close()
+
+
+@pytest.mark.parametrize("mode,depth,step_batch", [(X.MODE_LOWLAT, 2, 64), (X.MODE_LOWLAT, 4, 64),
+                                                   (X.MODE_LOWLAT, 3, 1024), (X.MODE_ZEROCOPY, 3, 64),
+                                                   (X.MODE_STAGED, 2, 256), (X.MODE_LOWLAT, 1, 64)])
+def test_rx_pipe_end_to_end(mode, depth, step_batch):
+    """The pipelined loop (xsk_gpu_rx_pipe_*): up to `depth` batches in flight, one per context, completed in RX order;
+    every frame, verdict and counter exactly xsk_gpu_rx_step's (the oracle's), nothing left in flight after the flush."""
+    _dev()
+    holder = {}
+
+    def step(umem, rx, fq, tx, pool, n, totals):
+        if "p" not in holder:
+            holder["p"] = X.RxPipe(umem, 0, depth=depth, mode=mode)
+        got, res = holder["p"].step(rx, fq, tx, pool, n, totals)
+        assert holder["p"].inflight <= depth
+        return got, res
+
+    def flush(tx, pool, totals):
+        got, res = holder["p"].flush(tx, pool, totals)
+        assert holder["p"].inflight == 0
+        return got, res
+
+    try:
+        _drive(step, flush, step_batch, depth * step_batch)
+    finally:
+        if "p" in holder:
+            holder["p"].close()
+
+
+def test_rx_pipe_partial_timeouts():
+    """Every batch of a pipelined LOWLAT loop times out half served -- each context's resident grid is launched one
+    workgroup wide while its batches are posted for two (xsk_gpu__lowlat_test_width) -- and completes through the
+    launch path: still every frame exact, in order, and the contexts' outcome counters show the partial services."""
+    _dev()
+    holder = {}
+
+    def step(umem, rx, fq, tx, pool, n, totals):
+        if "p" not in holder:
+            p = holder["p"] = X.RxPipe(umem, 0, depth=2, mode=X.MODE_LOWLAT)
+            for i in range(2):
+                c = p.context(i)
+                if c.mode == X.MODE_LOWLAT:
+                    c.lowlat_tune(groups=2, timeout_us=3000)
+                    c.lowlat_test_width(1)
+        return holder["p"].step(rx, fq, tx, pool, n, totals)
+
+    try:
+        _drive(step, lambda tx, pool, totals: holder["p"].flush(tx, pool, totals), 64, 2 * 64, n_pkts=3000)
+        lowlat = [holder["p"].context(i) for i in range(2) if holder["p"].context(i).mode == X.MODE_LOWLAT]
+        assert lowlat, "no LOWLAT slot on this device"
+        for c in lowlat:
+            oc = c.lowlat_outcomes()
+            assert oc["partial"] > 0 and oc["untouched"] == 0, oc
+    finally:
+        if "p" in holder:
+            holder["p"].close()

@@ -13,8 +13,10 @@
  * A step takes min(ring occupancy, step, XSK_GPU_RX_MAX_STEP) frames; the reference's RX_BATCH_SIZE (64,
  * src/lib/xsk_utils.h:8) is a constant of its CPU loop and changes no frame's result.
  *
- *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0]
+ *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0] [pipe=0]
  *
+ * pipe=D (1..XSK_GPU_RX_PIPE_MAX): the pipelined loop instead -- xsk_gpu_rx_pipe_step() with up to D batches in flight
+ * (one context each), a flush at the end; frames count when their batch completes.
  * empty=1: the empty-ring latency instead -- the NIC delivers exactly <step> frames, the step serves them, repeat
  * (each call finds exactly its batch: the RX-loop latency of tools/hostlat.py, through the ring loop).
  * Prints one JSON line: Mframes/s per queue and in total (frames / the timed application time), us per step (mean,
@@ -103,8 +105,10 @@ static void ring_init(struct xsk_gpu_ring* r, struct ring_mem* m, uint32_t size,
     if (producer_side) r->cached_cons = size; /* libxdp: a producer's cached consumer is consumer + size */
 }
 
+xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i); /* (library hook: a pipe's context) */
+
 struct queue {
-    uint32_t q, step, len, ring, frames, empty;
+    uint32_t q, step, len, ring, frames, empty, pipe;
     int mode, real_mode;
     double seconds;
     /* results */
@@ -143,10 +147,17 @@ static void* run_queue(void* arg) {
     pool.n_free = 0;
     for (uint32_t i = 0; i < F; i++) pool.addr[pool.n_free++] = (uint64_t)(F - 1 - i) * CHUNK; /* xsk_utils.c:140-141 */
     xsk_gpu_ctx* ctx = NULL;
+    xsk_gpu_rx_pipe* pipe = NULL;
     const uint32_t maxb = Q->step < XSK_GPU_RX_MAX_STEP ? Q->step : XSK_GPU_RX_MAX_STEP;
-    Q->rc = xsk_gpu_init(&ctx, 0, umem, (uint64_t)F * CHUNK, maxb, Q->mode);
-    if (Q->rc) return NULL;
-    Q->real_mode = xsk_gpu_ctx_mode(ctx);
+    if (Q->pipe) {
+        Q->rc = xsk_gpu_rx_pipe_init(&pipe, 0, umem, (uint64_t)F * CHUNK, Q->pipe, Q->mode);
+        if (Q->rc) return NULL;
+        Q->real_mode = xsk_gpu_ctx_mode(xsk_gpu__rx_pipe_ctx(pipe, Q->pipe - 1)); /* (the last may have no slot) */
+    } else {
+        Q->rc = xsk_gpu_init(&ctx, 0, umem, (uint64_t)F * CHUNK, maxb, Q->mode);
+        if (Q->rc) return NULL;
+        Q->real_mode = xsk_gpu_ctx_mode(ctx);
+    }
     /* the simulated kernel side: its own cursors over the shared index words */
     uint32_t k_rx_prod = 0, k_fill_cons = 0, k_tx_cons = 0, k_comp_prod = 0;
     struct xsk_gpu_stats st;
@@ -194,18 +205,31 @@ static void* run_queue(void* arg) {
         const double t0 = now_s();
         xsk_gpu_tx_complete(&comp, &pool, R);
         struct xsk_gpu_rx_result res;
-        const int got = xsk_gpu_rx_step(ctx, &rx, &fill, &tx, &pool, Q->step, &st, &res);
+        const int got = pipe ? xsk_gpu_rx_pipe_step(pipe, &rx, &fill, &tx, &pool, Q->step, &st, &res)
+                             : xsk_gpu_rx_step(ctx, &rx, &fill, &tx, &pool, Q->step, &st, &res);
         const double dt = now_s() - t0;
         if (got < 0) {
             Q->rc = got;
             break;
         }
-        if (got == 0) continue;
+        if (got == 0) {
+            if (pipe) Q->busy += dt; /* (a step that only posted) */
+            continue;
+        }
         if (res.replied != (uint32_t)got || res.tx_full) Q->fail += (uint64_t)got - res.replied;
         Q->busy += dt;
         Q->frames_done += (uint64_t)got;
         Q->steps++;
         Q->lat[Q->nlat++] = dt;
+    }
+    if (pipe) { /* the batches still in flight (timed: they are part of the run) */
+        const double t0 = now_s();
+        struct xsk_gpu_rx_result res;
+        const int got = xsk_gpu_rx_pipe_flush(pipe, &tx, &pool, &st, &res);
+        Q->busy += now_s() - t0;
+        if (got < 0) Q->rc = got;
+        else Q->frames_done += (uint64_t)got;
+        xsk_gpu_rx_pipe_fini(pipe);
     }
     xsk_gpu_fini(ctx);
     if (st.rx_packets != Q->frames_done || st.tx_packets != Q->frames_done) Q->fail++;
@@ -225,16 +249,17 @@ int main(int argc, char** argv) {
     const int mode = !strcmp(argv[2], "lowlat") ? XSK_GPU_MODE_LOWLAT
                      : !strcmp(argv[2], "staged") ? XSK_GPU_MODE_STAGED : XSK_GPU_MODE_ZEROCOPY;
     const double seconds = atof(argv[3]);
-    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0;
+    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0, pipe = 0;
     for (int a = 4; a < argc; a++) {
         if (!strncmp(argv[a], "len=", 4)) len = (uint32_t)atoi(argv[a] + 4);
         else if (!strncmp(argv[a], "queues=", 7)) nq = (uint32_t)atoi(argv[a] + 7);
         else if (!strncmp(argv[a], "ring=", 5)) ring = (uint32_t)atoi(argv[a] + 5);
         else if (!strncmp(argv[a], "frames=", 7)) frames = (uint32_t)atoi(argv[a] + 7);
         else if (!strncmp(argv[a], "empty=", 6)) empty = (uint32_t)atoi(argv[a] + 6);
+        else if (!strncmp(argv[a], "pipe=", 5)) pipe = (uint32_t)atoi(argv[a] + 5);
     }
     if (len < 42 || len > CHUNK - HEADROOM || nq < 1 || nq > 16 || (ring & (ring - 1)) || ring < 64 || frames < ring ||
-        step < 1) {
+        step < 1 || pipe > XSK_GPU_RX_PIPE_MAX) {
         fprintf(stderr, "bad arguments\n");
         return 2;
     }
@@ -248,6 +273,7 @@ int main(int argc, char** argv) {
         Q[q].ring = ring;
         Q[q].frames = frames;
         Q[q].empty = empty;
+        Q[q].pipe = pipe;
         Q[q].mode = mode;
         Q[q].seconds = seconds;
         pthread_create(&th[q], NULL, run_queue, &Q[q]);
@@ -256,7 +282,8 @@ int main(int argc, char** argv) {
     double busy_max = 0.0;
     int rc = 0;
     printf("{\"tool\": \"rxring\", \"step\": %u, \"mode\": \"%s\", \"len\": %u, \"queues\": %u, \"ring\": %u, "
-           "\"frames\": %u, \"empty\": %u, \"per_queue\": [", step, argv[2], len, nq, ring, frames, empty);
+           "\"frames\": %u, \"empty\": %u, \"pipe\": %u, \"per_queue\": [", step, argv[2], len, nq, ring, frames, empty,
+           pipe);
     for (uint32_t q = 0; q < nq; q++) {
         pthread_join(th[q], NULL);
         struct queue* R = &Q[q];

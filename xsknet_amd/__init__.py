@@ -128,6 +128,15 @@ _SIGS = {
     "xsk_gpu__lowlat_outcomes": ([_P, C.POINTER(C.c_uint64)], C.c_int),
     "xsk_gpu__lowlat_test_width": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu__multi_ctx": ([_P, C.c_uint32], _P),
+    "xsk_gpu__lowlat_live": ([C.c_int, C.POINTER(C.c_uint32)], C.c_int),
+    "xsk_gpu_rx_pipe_init": ([C.POINTER(_P), C.c_int, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
+    "xsk_gpu_rx_pipe_step": ([_P, C.POINTER(Ring), C.POINTER(Ring), C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32,
+                              _P, C.POINTER(RxResult)], C.c_int),
+    "xsk_gpu_rx_pipe_flush": ([_P, C.POINTER(Ring), C.POINTER(FramePool), _P, C.POINTER(RxResult)], C.c_int),
+    "xsk_gpu_rx_pipe_set_options": ([_P, C.c_uint32], C.c_int),
+    "xsk_gpu_rx_pipe_inflight": ([_P], C.c_uint32),
+    "xsk_gpu_rx_pipe_fini": ([_P], None),
+    "xsk_gpu__rx_pipe_ctx": ([_P, C.c_uint32], _P),
     # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
     "xsk_gpu__echo_dev_grid": ([_P, C.c_uint64, _P, C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint32], C.c_int),
 }
@@ -265,6 +274,13 @@ def timing_read():
     cnt = C.c_uint64(0)
     _check("xsk_gpu_timing_read", lib().xsk_gpu_timing_read(C.byref(ms), C.byref(cnt)))
     return ms.value, cnt.value
+
+
+def lowlat_live(device: int = 0) -> int:
+    """Workgroups of resident LOWLAT grids running on `device` in this process (xsk_gpu__lowlat_live)."""
+    out = C.c_uint32(0)
+    _check("xsk_gpu__lowlat_live", lib().xsk_gpu__lowlat_live(device, C.byref(out)))
+    return int(out.value)
 
 
 STAGED_FIELDS = ("h2d_bytes", "strided", "span", "gather", "contained", "hostpack", "own_dma")
@@ -424,6 +440,81 @@ class MultiContext:
         if self._ctx:
             lib().xsk_gpu_multi_fini(self._ctx)
             self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ContextView(EchoContext):
+    """A context owned by another object (a pipelined RX loop's): EchoContext's queries and test knobs, no ownership."""
+
+    def __init__(self, handle):  # noqa: super().__init__ is not called: nothing is created
+        self.umem = None
+        self._ctx = C.c_void_p(handle)
+
+    def close(self) -> None:
+        self._ctx = C.c_void_p()
+
+
+class RxPipe:
+    """xsk_gpu_rx_pipe_*: the RX loop step with up to ``depth`` batches in flight, one per context of ``mode`` over one
+    registration of the UMEM (include/xsk_gpu.h)."""
+
+    def __init__(self, umem: np.ndarray, device: int = 0, depth: int = 2, mode: int = MODE_LOWLAT, opts: int = 0):
+        assert umem.dtype == np.uint8 and umem.flags.c_contiguous
+        self.umem = umem
+        self.depth = depth
+        self._p = C.c_void_p()
+        _check("xsk_gpu_rx_pipe_init", lib().xsk_gpu_rx_pipe_init(C.byref(self._p), device, umem.ctypes.data,
+                                                                  umem.nbytes, depth, mode))
+        if opts:
+            self.set_options(opts)
+
+    def set_options(self, opts: int) -> None:
+        _check("xsk_gpu_rx_pipe_set_options", lib().xsk_gpu_rx_pipe_set_options(self._p, opts))
+
+    def step(self, rx: Ring, fill: Ring, tx: Ring, pool: FramePool, max_batch: int, stats=None):
+        """xsk_gpu_rx_pipe_step: returns (frames completed, RxResult)."""
+        res = RxResult()
+        rc = lib().xsk_gpu_rx_pipe_step(self._p, C.byref(rx), C.byref(fill), C.byref(tx), C.byref(pool), max_batch,
+                                        stats.ctypes.data if stats is not None else None, C.byref(res))
+        if rc < 0:
+            raise XskGpuError("xsk_gpu_rx_pipe_step", rc)
+        return rc, res
+
+    def flush(self, tx: Ring, pool: FramePool, stats=None):
+        """xsk_gpu_rx_pipe_flush: returns (frames completed, RxResult)."""
+        res = RxResult()
+        rc = lib().xsk_gpu_rx_pipe_flush(self._p, C.byref(tx), C.byref(pool),
+                                         stats.ctypes.data if stats is not None else None, C.byref(res))
+        if rc < 0:
+            raise XskGpuError("xsk_gpu_rx_pipe_flush", rc)
+        return rc, res
+
+    @property
+    def inflight(self) -> int:
+        return int(lib().xsk_gpu_rx_pipe_inflight(self._p))
+
+    def context(self, i: int) -> ContextView:
+        """Context i of the pipe (xsk_gpu__rx_pipe_ctx): its mode, LOWLAT knobs and outcomes."""
+        h = lib().xsk_gpu__rx_pipe_ctx(self._p, i)
+        if not h:
+            raise XskGpuError("xsk_gpu__rx_pipe_ctx", -22)
+        return ContextView(h)
+
+    def close(self) -> None:
+        if self._p:
+            lib().xsk_gpu_rx_pipe_fini(self._p)
+            self._p = C.c_void_p()
 
     def __enter__(self):
         return self

@@ -84,6 +84,12 @@ struct xsk_gpu_ctx {
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
     uint64_t ll_outcome[3]; /* LOWLAT doorbell batches that timed out: all, completed through the launch path after a
                              * partial service, returned -ETIMEDOUT (xsk_gpu__lowlat_outcomes) */
+    /* the batch xsk_gpu__submit put in flight and xsk_gpu__complete has not taken back yet */
+    uint32_t pend_n;      /* its frames; 0: none */
+    int pend_bell;        /* on the doorbell (else launched) */
+    uint32_t pend_w;      /* doorbell: its serving workgroups */
+    uint32_t pend_chunks; /* launched: its chunks */
+    int pend_recs;        /* records asked for */
 };
 
 /* LOWLAT contexts per device in this process (include/xsk_gpu.h, XSK_GPU_LOWLAT_PER_DEVICE): a slot is taken at
@@ -162,6 +168,7 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
 
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (!c) return;
+    (void)xsk_gpu__complete(c, NULL, NULL, NULL); /* a batch still in flight: let it finish (results dropped) */
     (void)hipSetDevice(c->device);
     xsk_gpu__lowlat_free(c->ll); /* stops the resident kernel (waits for it) ... */
     if (c->ll_slot) ll_slot_give(c->device); /* ... before its hardware queue is offered to another context */
@@ -311,7 +318,7 @@ int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t ume
 uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* c) { return c ? c->max_batch : 0u; }
 
 void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* c) {
-    if (!c || !c->ll) return;
+    if (!c || !c->ll || c->pend_n) return; /* (never with a batch in flight: its completion must see it served) */
     (void)hipSetDevice(c->device);
     xsk_gpu__lowlat_stop(c->ll);
 }
@@ -339,6 +346,7 @@ xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; 
 
 int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     if (!c || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
+    if (c->pend_n) return -EBUSY; /* the batch in flight runs under the options it was submitted with */
     if (c->ll) {
         (void)hipSetDevice(c->device);
         const int rc = xsk_gpu__lowlat_set_opts(c->ll, opts);
@@ -516,8 +524,15 @@ int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
 
 int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n, uint8_t* verdicts,
                         struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats, int no_doorbell) {
+    const int rc = xsk_gpu__submit(c, descs, n, recs != NULL, no_doorbell);
+    if (rc) return rc;
+    return xsk_gpu__complete(c, verdicts, recs, stats);
+}
+
+int xsk_gpu__submit(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n, int want_recs, int no_doorbell) {
     int rc = 0;
     if (!c || (!descs && n)) return -EINVAL;
+    if (c->pend_n) return -EBUSY; /* one batch in flight per context */
     if (n == 0) return 0;
     if (n > c->max_batch) return -EINVAL;
     if (c->ll && xsk_gpu__lowlat_broken(c->ll)) {
@@ -527,41 +542,13 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
     }
     if (c->ll && n <= XSK_GPU_LOWLAT_MAX && !no_doorbell) { /* the doorbell: no launch, no sync, no HIP call */
         memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
-        uint32_t w = 0, unserved = 0;
-        rc = xsk_gpu__lowlat_run(c->ll, n, recs != NULL, &w, &unserved);
-        /* timed out: untouched frames stay the caller's (-ETIMEDOUT) unless the channel stopped with part of the
-         * batch served -- the GPU is evidently alive, so the untouched slices take the launch path and the call
-         * completes, every frame transformed exactly once */
-        const int partial = rc == -ETIMEDOUT && !xsk_gpu__lowlat_broken(c->ll) && unserved &&
-                            unserved != (1u << w) - 1u;
-        if (rc == -ETIMEDOUT) c->ll_outcome[partial ? 1 : 2]++, c->ll_outcome[0]++;
-        if (rc && !partial) return rc;
-        uint8_t hv[XSK_GPU_LOWLAT_MAX];
-        memcpy(hv, xsk_gpu__lowlat_verdicts(c->ll), n);
-        if (recs) memcpy(recs, xsk_gpu__lowlat_recs(c->ll), (size_t)n * sizeof *recs);
-        for (uint32_t g = 0; partial && g < w; g++) {
-            if (!((unserved >> g) & 1u)) continue;
-            uint32_t f0 = 0, f1 = 0;
-            xsk_gpu__ll_slice(n, w, g, &f0, &f1);
-            if (f1 <= f0) continue;
-            rc = xsk_gpu__process_ex(c, descs + f0, f1 - f0, hv + f0, recs ? recs + f0 : NULL, NULL, 1);
-            if (rc) return rc;
-        }
-        if (verdicts) memcpy(verdicts, hv, n);
-        if (stats) { /* xsk_receive.c:171-172, 229, 233 -- what the kernel's counter phase would add */
-            uint64_t rxb = 0, txp = 0, txb = 0;
-            for (uint32_t i = 0; i < n; i++) {
-                rxb += descs[i].len;
-                if (hv[i] == XSK_GPU_TX_REPLY) {
-                    txp++;
-                    txb += descs[i].len;
-                }
-            }
-            stats->rx_packets += n;
-            stats->rx_bytes += rxb;
-            stats->tx_packets += txp;
-            stats->tx_bytes += txb;
-        }
+        uint32_t w = 0;
+        rc = xsk_gpu__lowlat_post(c->ll, n, want_recs, &w);
+        if (rc) return rc;
+        c->pend_n = n;
+        c->pend_bell = 1;
+        c->pend_w = w;
+        c->pend_recs = want_recs;
         return 0;
     }
     int caller_dev = -1; /* the caller's current device, restored on return */
@@ -573,17 +560,91 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
     int prefix_aligned = 1; /* every frame of the chunks enqueued so far starts 16-B aligned */
     for (uint32_t i0 = 0; i0 < n; nchunks++) {
         const uint32_t m = staged ? stage_chunk(n, n - i0) : n;
-        rc = enqueue_chunk(c, descs, i0, m, nchunks, recs != NULL, (int)(nchunks % NSTREAMS), &prefix_aligned);
-        if (rc) goto drain;
+        rc = enqueue_chunk(c, descs, i0, m, nchunks, want_recs, (int)(nchunks % NSTREAMS), &prefix_aligned);
+        if (rc) {
+            for (int s = 0; s < NSTREAMS; s++) (void)hipStreamSynchronize(c->stream[s]);
+            goto out;
+        }
         i0 += m;
     }
-    for (uint32_t ci = 0, i0 = 0; ci < nchunks; ci++) {
+    c->pend_n = n;
+    c->pend_bell = 0;
+    c->pend_chunks = nchunks;
+    c->pend_recs = want_recs;
+out:
+    if (caller_dev >= 0 && caller_dev != c->device) (void)hipSetDevice(caller_dev);
+    return rc;
+}
+
+int xsk_gpu__ready(const xsk_gpu_ctx* c) {
+    if (!c || !c->pend_n) return 1;
+    if (c->pend_bell) return xsk_gpu__lowlat_ready(c->ll);
+    return hipEventQuery(c->done[c->pend_chunks - 1]) == hipSuccess;
+}
+
+/* The doorbell batch in flight: wait, then verdicts, records and the counters the kernel's counter phase would add. */
+static int complete_doorbell(xsk_gpu_ctx* c, uint32_t n, uint8_t* verdicts, struct xsk_gpu_rec* recs,
+                             struct xsk_gpu_stats* stats) {
+    const struct xsk_gpu_desc* descs = xsk_gpu__lowlat_descs(c->ll); /* the batch as submitted (options aside) */
+    const uint32_t w = c->pend_w;
+    if (!c->pend_recs) recs = NULL;
+    uint32_t unserved = 0;
+    int rc = xsk_gpu__lowlat_wait(c->ll, &unserved);
+    /* timed out: untouched frames stay the caller's (-ETIMEDOUT) unless the channel stopped with part of the
+     * batch served -- the GPU is evidently alive, so the untouched slices take the launch path and the call
+     * completes, every frame transformed exactly once */
+    const int partial = rc == -ETIMEDOUT && !xsk_gpu__lowlat_broken(c->ll) && unserved && unserved != (1u << w) - 1u;
+    if (rc == -ETIMEDOUT) c->ll_outcome[partial ? 1 : 2]++, c->ll_outcome[0]++;
+    if (rc && !partial) return rc;
+    uint8_t hv[XSK_GPU_LOWLAT_MAX];
+    memcpy(hv, xsk_gpu__lowlat_verdicts(c->ll), n);
+    if (recs) memcpy(recs, xsk_gpu__lowlat_recs(c->ll), (size_t)n * sizeof *recs);
+    for (uint32_t g = 0; partial && g < w; g++) {
+        if (!((unserved >> g) & 1u)) continue;
+        uint32_t f0 = 0, f1 = 0;
+        xsk_gpu__ll_slice(n, w, g, &f0, &f1);
+        if (f1 <= f0) continue;
+        rc = xsk_gpu__process_ex(c, descs + f0, f1 - f0, hv + f0, recs ? recs + f0 : NULL, NULL, 1);
+        if (rc) return rc;
+    }
+    if (verdicts) memcpy(verdicts, hv, n);
+    if (stats) { /* xsk_receive.c:171-172, 229, 233 -- what the kernel's counter phase would add */
+        uint64_t rxb = 0, txp = 0, txb = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            rxb += descs[i].len;
+            if (hv[i] == XSK_GPU_TX_REPLY) {
+                txp++;
+                txb += descs[i].len;
+            }
+        }
+        stats->rx_packets += n;
+        stats->rx_bytes += rxb;
+        stats->tx_packets += txp;
+        stats->tx_bytes += txb;
+    }
+    return 0;
+}
+
+int xsk_gpu__complete(xsk_gpu_ctx* c, uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats) {
+    int rc = 0;
+    if (!c) return -EINVAL;
+    const uint32_t n = c->pend_n;
+    if (!n) return 0;
+    c->pend_n = 0;
+    if (c->pend_bell) return complete_doorbell(c, n, verdicts, recs, stats);
+    if (!c->pend_recs) recs = NULL;
+    const struct xsk_gpu_desc* descs = c->h_descs; /* the batch as submitted: every chunk copied it there */
+    int caller_dev = -1;
+    if (hipGetDevice(&caller_dev) != hipSuccess) caller_dev = -1;
+    TRY(hipSetDevice(c->device));
+    const int staged = c->mode == XSK_GPU_MODE_STAGED;
+    for (uint32_t ci = 0, i0 = 0; ci < c->pend_chunks; ci++) {
         const uint32_t m = staged ? stage_chunk(n, n - i0) : n;
         if (hipEventSynchronize(c->done[ci]) != hipSuccess) {
             rc = -EIO;
             goto drain;
         }
-        if (c->mode == XSK_GPU_MODE_STAGED) { /* scatter the rewritten bytes of this chunk's replies */
+        if (staged) { /* scatter the rewritten bytes of this chunk's replies */
             for (uint32_t i = i0; i < i0 + m; i++) {
                 if (c->h_verd[i] != XSK_GPU_TX_REPLY) continue;
                 /* reference mode rewrites bytes [0, 38); wire mode bytes below l4 + 4 <= 86 <= len */

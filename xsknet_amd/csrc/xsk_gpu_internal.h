@@ -113,6 +113,29 @@ XSK_GPU__HIDDEN int xsk_gpu__process_ex(xsk_gpu_ctx* ctx, const struct xsk_gpu_d
                                         uint8_t* verdicts, struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats,
                                         int no_doorbell);
 
+/* xsk_gpu_host.c: xsk_gpu__process_ex in two halves, so that a caller with several contexts keeps a batch in flight on
+ * each (the pipelined RX loop, xsk_gpu_pipe.c).  submit enqueues the batch -- posts it on the doorbell, or launches it
+ * -- and returns (-EBUSY while the context has one in flight; the descriptors are copied, `descs` may be reused at
+ * once); complete waits for it and returns what xsk_gpu_process would have (0 with nothing in flight); ready = complete
+ * would not block.  Records come back only when submit asked for them. */
+XSK_GPU__HIDDEN int xsk_gpu__submit(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc* descs, uint32_t n, int want_recs,
+                                    int no_doorbell);
+XSK_GPU__HIDDEN int xsk_gpu__complete(xsk_gpu_ctx* ctx, uint8_t* verdicts, struct xsk_gpu_rec* recs,
+                                      struct xsk_gpu_stats* stats);
+XSK_GPU__HIDDEN int xsk_gpu__ready(const xsk_gpu_ctx* ctx);
+
+/* xsk_gpu_rx.c, shared by xsk_gpu_rx_step and the pipelined loop (xsk_gpu_pipe.c): stock the fill ring from the
+ * free-frame stack (src/lib/xsk_receive.c:201-217; returns the frames handed over), and hand a transformed batch on --
+ * replies onto the TX ring while it has room, every other frame back to the pool, the counters (:171-186, :226-233);
+ * r->replied and r->tx_full accumulate. */
+XSK_GPU__HIDDEN uint32_t xsk_gpu__rx_refill(struct xsk_gpu_ring* fill, struct xsk_gpu_frame_pool* pool);
+XSK_GPU__HIDDEN void xsk_gpu__rx_emit(const struct xsk_gpu_desc* descs, const uint8_t* verdict, uint32_t n,
+                                      struct xsk_gpu_ring* tx, struct xsk_gpu_frame_pool* pool,
+                                      struct xsk_gpu_stats* stats, struct xsk_gpu_rx_result* r);
+
+/* xsk_gpu_pipe.c (tests and tools, not part of the ABI): context i of a pipelined RX loop, or NULL. */
+xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i);
+
 /* xsk_gpu_multi.c (exported for the GPU tests, not part of the ABI): context g's next share fails with `rc`
  * without being processed (fault injection for the partial-failure semantics). */
 int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
@@ -168,6 +191,11 @@ XSK_GPU__HIDDEN void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll);
  * slices left untouched (all bits when the channel is broken: unknown). */
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups,
                                         uint32_t* unserved);
+/* The two halves of xsk_gpu__lowlat_run (xsk_gpu__ll_begin / xsk_gpu__ll_wait): post the batch (-EBUSY while one is in
+ * flight), wait for the one in flight; ready = it is complete (never blocks). */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_post(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups);
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_wait(xsk_gpu__lowlat* ll, uint32_t* unserved);
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_ready(const xsk_gpu__lowlat* ll);
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts);
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
 /* 1 while a timed-out batch's instance has not stopped (later calls return -EBUSY). */
@@ -199,6 +227,10 @@ int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* ctx, uint64_t out[3]);
  * asks (xsk_gpu__lowlat_tune's `groups`): slices of workgroups that do not exist are never served, which makes a batch
  * time out partly served -- the deterministic test of the partial-timeout path. */
 int xsk_gpu__lowlat_test_width(xsk_gpu_ctx* ctx, uint32_t wgs);
+/* xsk_lowlat.hip (exported for the GPU tests, not part of the ABI): workgroups of resident LOWLAT grids running on
+ * `device` in this process right now (each adds itself when it starts and leaves when it exits): 0 once every LOWLAT
+ * context is gone -- no grid outlives its channel. */
+int xsk_gpu__lowlat_live(int device, uint32_t* out);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,53 @@ static inline void pool_push(struct xsk_gpu_frame_pool* p, uint64_t a) {
     if (p->n_free < p->capacity) p->addr[p->n_free++] = a; /* xsk_free_umem_frame (:65-70) */
 }
 
+uint32_t xsk_gpu__rx_refill(struct xsk_gpu_ring* fill, struct xsk_gpu_frame_pool* pool) {
+    uint32_t stock = xr_prod_free(fill, pool->n_free);
+    if (stock > pool->n_free) stock = pool->n_free;
+    if (!stock) return 0;
+    uint32_t idx_fq = 0;
+    if (xr_prod_reserve(fill, stock, &idx_fq) != stock) return 0;
+    for (uint32_t i = 0; i < stock; i++) *xr_addr(fill, idx_fq + i) = pool->addr[--pool->n_free];
+    xr_prod_submit(fill, stock);
+    return stock;
+}
+
+void xsk_gpu__rx_emit(const struct xsk_gpu_desc* descs, const uint8_t* verdict, uint32_t n, struct xsk_gpu_ring* tx,
+                      struct xsk_gpu_frame_pool* pool, struct xsk_gpu_stats* stats, struct xsk_gpu_rx_result* r) {
+    uint32_t nrep = 0;
+    for (uint32_t i = 0; i < n; i++) nrep += verdict[i] == XSK_GPU_TX_REPLY;
+    /* :174-186 — replies onto the TX ring, as many as it has room for */
+    uint32_t idx_tx = 0, room = 0, sent = 0;
+    if (nrep) {
+        room = xr_prod_free(tx, nrep);
+        if (room > nrep) room = nrep;
+        if (room) xr_prod_reserve(tx, room, &idx_tx);
+    }
+    uint64_t rx_bytes = 0, tx_bytes = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        rx_bytes += descs[i].len;
+        if (verdict[i] == XSK_GPU_TX_REPLY && sent < room) {
+            struct xsk_gpu_desc* t = xr_desc(tx, idx_tx + sent);
+            t->addr = descs[i].addr;
+            t->len = descs[i].len;
+            t->options = 0;
+            sent++;
+            tx_bytes += descs[i].len;
+        } else {
+            if (verdict[i] == XSK_GPU_TX_REPLY) r->tx_full++;
+            pool_push(pool, descs[i].addr); /* :226-227 */
+        }
+    }
+    if (sent) xr_prod_submit(tx, sent);
+    r->replied += sent;
+    if (stats) {
+        stats->rx_packets += n;        /* :233 */
+        stats->rx_bytes += rx_bytes;   /* :229 */
+        stats->tx_packets += sent;     /* :172 */
+        stats->tx_bytes += tx_bytes;   /* :171 */
+    }
+}
+
 int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ring* fill, struct xsk_gpu_ring* tx,
                     struct xsk_gpu_frame_pool* pool, uint32_t max_batch, struct xsk_gpu_stats* stats,
                     struct xsk_gpu_rx_result* res) {
@@ -32,59 +79,18 @@ int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ri
 
     uint32_t idx_rx = 0;
     const uint32_t rcvd = xr_cons_peek(rx, max_batch, &idx_rx); /* :196 */
-    /* :201-217 — stock the fill ring from the free-frame stack */
-    uint32_t stock = xr_prod_free(fill, pool->n_free);
-    if (stock > pool->n_free) stock = pool->n_free;
-    if (stock) {
-        uint32_t idx_fq = 0;
-        if (xr_prod_reserve(fill, stock, &idx_fq) == stock) {
-            for (uint32_t i = 0; i < stock; i++) *xr_addr(fill, idx_fq + i) = pool->addr[--pool->n_free];
-            xr_prod_submit(fill, stock);
-            r.refilled = stock;
-        }
-    }
+    r.refilled = xsk_gpu__rx_refill(fill, pool);                /* :201-217 */
     /* :222-223 — the batch's descriptors */
     for (uint32_t i = 0; i < rcvd; i++) descs[i] = *xr_desc(rx, idx_rx + i);
 
-    struct xsk_gpu_stats st;
-    memset(&st, 0, sizeof st);
-    const int rc = xsk_gpu_process(ctx, descs, rcvd, verdict, NULL, &st);
+    const int rc = xsk_gpu_process(ctx, descs, rcvd, verdict, NULL, NULL);
     if (rc) { /* frames stay on the RX ring (not released); the caller may retry or tear down */
         rx->cached_cons -= rcvd;
         return rc;
     }
-    uint32_t nrep = 0;
-    for (uint32_t i = 0; i < rcvd; i++) nrep += verdict[i] == XSK_GPU_TX_REPLY;
-    /* :174-186 — replies onto the TX ring, as many as it has room for */
-    uint32_t idx_tx = 0, room = 0;
-    if (nrep) {
-        room = xr_prod_free(tx, nrep);
-        if (room > nrep) room = nrep;
-        if (room) xr_prod_reserve(tx, room, &idx_tx);
-    }
-    uint64_t tx_bytes = 0;
-    for (uint32_t i = 0; i < rcvd; i++) {
-        if (verdict[i] == XSK_GPU_TX_REPLY && r.replied < room) {
-            struct xsk_gpu_desc* t = xr_desc(tx, idx_tx + r.replied);
-            t->addr = descs[i].addr;
-            t->len = descs[i].len;
-            t->options = 0;
-            r.replied++;
-            tx_bytes += descs[i].len;
-        } else {
-            if (verdict[i] == XSK_GPU_TX_REPLY) r.tx_full++;
-            pool_push(pool, descs[i].addr); /* :226-227 */
-        }
-    }
-    if (r.replied) xr_prod_submit(tx, r.replied);
+    xsk_gpu__rx_emit(descs, verdict, rcvd, tx, pool, stats, &r);
     xr_cons_release(rx, rcvd); /* :232 */
     r.received = rcvd;
-    if (stats) {
-        stats->rx_packets += rcvd;       /* :233 */
-        stats->rx_bytes += st.rx_bytes;  /* :229 */
-        stats->tx_packets += r.replied;  /* :172 */
-        stats->tx_bytes += tx_bytes;     /* :171 */
-    }
     if (res) *res = r;
     return (int)rcvd;
 }

@@ -48,6 +48,10 @@ constexpr int kLLSync = 0;                   // one round: write as soon as the 
 
 constexpr int kPollCopies = 2;  // doorbell words (and first-64 descriptor blocks) polled in turn
 
+// workgroups of resident grids running now, in this process (device memory; each workgroup adds one when it starts
+// and takes it back when it leaves): xsk_gpu__lowlat_live, the tests' check that no grid outlives its channel
+__device__ unsigned int g_ll_live;
+
 struct LowlatArgs {
     xsk_gpu__bell* bell;  // device alias of the mapped doorbell
     xsk_gpu__lldiag* diag;  // device memory
@@ -216,6 +220,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
     const uint32_t g = blockIdx.x;
     const bool leader = g == 0;
     PollState P = {};  // wave 0: `served`, the two polls' registers, diagnostics
+    if (threadIdx.x == 0) atomicAdd(&g_ll_live, 1u);
     if (threadIdx.x < 64) {  // wave 0 polls; every lane keeps the same `served`
         // this workgroup's last completed batch (a previous instance's; stream order: it has exited)
         P.served = uniform(ld_sys(&bell->wg[g].done));
@@ -293,6 +298,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
             }
         }
     }
+    if (threadIdx.x == 0) atomicSub(&g_ll_live, 1u);
 }
 
 }  // namespace
@@ -310,6 +316,7 @@ struct xsk_gpu__lowlat {
     uint32_t tile_q;       // frames per wave / 4 (0: from the slice's bytes); xsk_gpu__lowlat_tune
     uint32_t groups;       // serving workgroups (0: xsk_gpu__ll_groups); xsk_gpu__lowlat_tune
     uint64_t host_ns[2];   // last batch on the host: entry -> doorbell posted, posted -> completion seen
+    double h_enter, h_post; // the batch in flight: entry, doorbell posted
     uint32_t width;        // workgroups a launch starts (0: XSK_GPU__LL_WG); xsk_gpu__lowlat_test_width
 };
 
@@ -410,6 +417,12 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, dfl));
     LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), dfl));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
+    // the descriptor slots too: the leader takes a polled slot as this batch's when its `options` tag equals the
+    // batch's seq, and a recycled allocation may still hold an earlier channel's slots tagged 1, 2, 3, ... -- the seqs
+    // this channel starts with.  A poll that read such a slot before the host's new one landed took the old channel's
+    // descriptors for its own (seen once the pipelined loop made channels come and go: wrong verdicts, frames
+    // untouched).  Zeroed, a slot's tag is never a posted seq (seqs start at 1).
+    memset((void*)ll->h_descs, 0, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc));
     LL_TRY(hipMalloc((void**)&ll->d_diag, sizeof(xsk_gpu__lldiag)));
     LL_TRY(hipMemset(ll->d_diag, 0, sizeof(xsk_gpu__lldiag)));
     LowlatArgs& A = ll->args;
@@ -439,11 +452,11 @@ int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts) {
     return 0;
 }
 
-int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups, uint32_t* unserved) {
+int xsk_gpu__lowlat_post(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups) {
     if (groups) *groups = 0;
-    if (unserved) *unserved = 0;
     if (!ll || n > XSK_GPU_LOWLAT_MAX) return -EINVAL;
-    const double h_enter = ll_now(nullptr);
+    if (ll->st.inflight) return -EBUSY;
+    ll->h_enter = ll_now(nullptr);
     if (ll->st.broken && !ll_stream_idle(ll)) return -EBUSY;  // before touching the slots it may still read
     const uint32_t w = ll->groups ? (ll->groups < n ? ll->groups : (n ? n : 1u)) : xsk_gpu__ll_groups(ll->h_descs, n);
     uint32_t f0 = 0, f1 = 0;
@@ -459,16 +472,31 @@ int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t
         shadow[i] = ll->h_descs[i];
     }
     const xsk_gpu__ll_ops o = ll_ops(ll);
-    const double h_post = ll_now(nullptr);
+    ll->h_post = ll_now(nullptr);
     if (groups) *groups = w;
-    const int rc = xsk_gpu__ll_run(&ll->st, &o,
-                                   XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) | XSK_GPU__BELL_TILE(tq), w,
-                                   unserved);
+    return xsk_gpu__ll_begin(&ll->st, &o,
+                             XSK_GPU__BELL_N(n) | (want_recs ? XSK_GPU__BELL_RECS : 0ull) | XSK_GPU__BELL_TILE(tq), w);
+}
+
+int xsk_gpu__lowlat_wait(xsk_gpu__lowlat* ll, uint32_t* unserved) {
+    if (unserved) *unserved = 0;
+    if (!ll) return -EINVAL;
+    const xsk_gpu__ll_ops o = ll_ops(ll);
+    const int rc = xsk_gpu__ll_wait(&ll->st, &o, unserved);
     if (rc) return rc;
     const double h_done = ll_now(nullptr);
-    ll->host_ns[0] = (uint64_t)((h_post - h_enter) * 1e9);
-    ll->host_ns[1] = (uint64_t)((h_done - h_post) * 1e9);
+    ll->host_ns[0] = (uint64_t)((ll->h_post - ll->h_enter) * 1e9);
+    ll->host_ns[1] = (uint64_t)((h_done - ll->h_post) * 1e9);
     return 0;
+}
+
+int xsk_gpu__lowlat_ready(const xsk_gpu__lowlat* ll) { return ll && xsk_gpu__ll_ready(&ll->st); }
+
+int xsk_gpu__lowlat_run(xsk_gpu__lowlat* ll, uint32_t n, int want_recs, uint32_t* groups, uint32_t* unserved) {
+    if (unserved) *unserved = 0;
+    const int rc = xsk_gpu__lowlat_post(ll, n, want_recs, groups);
+    if (rc) return rc;
+    return xsk_gpu__lowlat_wait(ll, unserved);
 }
 
 struct xsk_gpu_desc* xsk_gpu__lowlat_descs(xsk_gpu__lowlat* ll) { return ll->h_descs; }
@@ -512,5 +540,23 @@ int xsk_gpu__lowlat_test_width(xsk_gpu_ctx* ctx, uint32_t wgs) {
 }
 
 void xsk_gpu__lowlat_free(xsk_gpu__lowlat* ll) { ll_free(ll); }
+
+int xsk_gpu__lowlat_live(int device, uint32_t* out) {
+    if (!out) return -EINVAL;
+    *out = 0;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (hipSetDevice(device) != hipSuccess) return -ENODEV;
+    // its own non-blocking stream: the null stream could wait behind a resident grid
+    hipStream_t st = nullptr;
+    int rc = 0;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+        hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_ll_live), sizeof *out, 0, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        rc = -EIO;
+    if (st) (void)hipStreamDestroy(st);
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+}
 
 }  // extern "C"

@@ -118,6 +118,9 @@ struct xsk_gpu__ll_state {
     double timeout_s;     /* a batch not complete after this long: -ETIMEDOUT */
     double quiesce_s;     /* after a timeout, how long to wait for the instance to stop */
     double recheck_s;     /* while waiting, how often to check that an instance is still there */
+    int inflight;         /* xsk_gpu__ll_begin posted seq and xsk_gpu__ll_wait has not returned for it yet */
+    uint32_t w_post;      /* its serving workgroups */
+    double t_post;        /* when it was posted */
 };
 
 static inline void xsk_gpu__ll_post(struct xsk_gpu__bell* b, uint64_t c) {
@@ -148,8 +151,10 @@ static inline uint32_t xsk_gpu__ll_unserved(const struct xsk_gpu__bell* b, uint3
  * word (its seq, n and workgroup fields kept, so a workgroup that has not taken that batch yet retires exactly its
  * own slice unserved), and wait up to `wait_s` (< 0: for ever) for the stream to drain.  Returns 0 once no instance
  * runs -- the last batch then retired for every workgroup -- or -ETIMEDOUT if one still did at the deadline (the
- * channel is then `broken`). */
+ * channel is then `broken`).  A batch still in flight (posted, not waited for) ends here: stop_unserved says what was
+ * done with it. */
 static inline int xsk_gpu__ll_stop(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, double wait_s) {
+    st->inflight = 0;
     if (!st->launched && !st->broken) return 0;
     xsk_gpu__ll_post(st->bell, (st->cmd & ~0xFFFFFFFFull) | (uint64_t)st->seq | XSK_GPU__BELL_STOP);
     const double t0 = ops->now(ops->u);
@@ -171,23 +176,32 @@ static inline int xsk_gpu__ll_stop(struct xsk_gpu__ll_state* st, const struct xs
     }
 }
 
-/* One doorbell batch: the caller has written the descriptors (slots 0 .. n-1, the `options` of the first 64
- * tagged with seq + 1, the seq this call posts) into the mapped buffer.  `bits` = the n / records / tile fields; w = serving
- * workgroups.  Returns 0 when every serving workgroup has published completion (the caller's outputs are
- * then in the mapped buffers), or:
- *   -EBUSY      an earlier call timed out and its instance has still not stopped: nothing was posted;
- *   -ETIMEDOUT  the batch did not complete within timeout_s: STOP was posted and the instance waited for
+/* One doorbell batch, in two halves (xsk_gpu__ll_run = begin + wait; a caller with several channels keeps one batch in
+ * flight on each -- the pipelined RX loop, xsk_gpu_pipe.c).
+ *
+ * xsk_gpu__ll_begin posts it: the caller has written the descriptors (slots 0 .. n-1, the `options` of the first 64
+ * tagged with seq + 1, the seq this call posts) into the mapped buffer.  `bits` = the n / records / tile fields; w =
+ * serving workgroups.  Returns 0 when the batch is posted (then xsk_gpu__ll_wait must follow before anything else is
+ * posted on this channel), or:
+ *   -EBUSY      an earlier batch timed out and its instance has still not stopped, or a batch is still in flight:
+ *               nothing was posted;
+ *   a launch error.
+ *
+ * xsk_gpu__ll_wait returns 0 when every serving workgroup has published completion (the caller's outputs are then
+ * in the mapped buffers), or:
+ *   -ETIMEDOUT  the batch did not complete within timeout_s of its post: STOP was posted and the instance waited for
  *               (quiesce_s).  Once it has stopped, every slice is either transformed exactly once or untouched
  *               (a workgroup that finds STOP with a batch it has not taken retires it unserved), *unserved says
  *               which slices are untouched (bit g: slice g of xsk_gpu__ll_slice), and no later instance serves the
  *               batch; if every slice turned out to be served the call returns 0 after all.  If the instance had not
- *               stopped by then, the channel stays `broken`, *unserved has every bit set (unknown), and later calls
+ *               stopped by then, the channel stays `broken`, *unserved has every bit set (unknown), and later posts
  *               return -EBUSY until it has;
+ *   -EINVAL     nothing in flight;
  *   a launch error. */
-static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, uint64_t bits,
-                                  uint32_t w, uint32_t* unserved) {
+static inline int xsk_gpu__ll_begin(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, uint64_t bits,
+                                    uint32_t w) {
     struct xsk_gpu__bell* b = st->bell;
-    if (unserved) *unserved = 0;
+    if (st->inflight) return -EBUSY;
     if (st->broken) {
         if (!ops->stream_idle(ops->u)) return -EBUSY;
         xsk_gpu__ll_retire(st); /* the stopped instance's batch is never served by a relaunch */
@@ -210,9 +224,30 @@ static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk
         /* the leader was leaving (Dekker: it re-reads the doorbell after clearing alive, or this launch serves
          * the batch) */
         const int rc = ops->launch(ops->u);
-        if (rc) return rc;
+        if (rc) return rc; /* (posted, maybe never served: the next stop / relaunch retires or serves it) */
     }
-    const double t_post = ops->now(ops->u);
+    st->inflight = 1;
+    st->w_post = w;
+    st->t_post = ops->now(ops->u);
+    return 0;
+}
+
+/* The batch in flight is complete (never blocks; 0 while it is not or when nothing is in flight). */
+static inline int xsk_gpu__ll_ready(const struct xsk_gpu__ll_state* st) {
+    if (!st->inflight) return 0;
+    for (uint32_t g = 0; g < st->w_post; g++)
+        if (__atomic_load_n(&st->bell->wg[g].done, __ATOMIC_ACQUIRE) != st->seq) return 0;
+    return 1;
+}
+
+static inline int xsk_gpu__ll_wait(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops,
+                                   uint32_t* unserved) {
+    struct xsk_gpu__bell* b = st->bell;
+    if (unserved) *unserved = 0;
+    if (!st->inflight) return -EINVAL;
+    st->inflight = 0; /* whatever happens below, the batch leaves the channel's hands */
+    const uint32_t seq = st->seq, w = st->w_post;
+    const double t_post = st->t_post;
     double t_check = t_post;
     for (uint32_t spin = 0;; ++spin) {
         uint32_t g = 0;
@@ -248,6 +283,15 @@ static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     return 0;
+}
+
+/* Post one batch and wait for it (the returns of both halves above). */
+static inline int xsk_gpu__ll_run(struct xsk_gpu__ll_state* st, const struct xsk_gpu__ll_ops* ops, uint64_t bits,
+                                  uint32_t w, uint32_t* unserved) {
+    if (unserved) *unserved = 0;
+    const int rc = xsk_gpu__ll_begin(st, ops, bits, w);
+    if (rc) return rc;
+    return xsk_gpu__ll_wait(st, ops, unserved);
 }
 
 #ifdef __cplusplus
