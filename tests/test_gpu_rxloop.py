@@ -160,60 +160,3 @@ def test_rx_loop_end_to_end(mode, ctx_batch, step_batch):
     finally:
         if "ctx" in holder:
             holder["ctx"].close()
-
-
-@pytest.mark.parametrize("mode,depth,step_batch", [(X.MODE_LOWLAT, 2, 64), (X.MODE_LOWLAT, 4, 64),
-                                                   (X.MODE_LOWLAT, 3, 1024), (X.MODE_ZEROCOPY, 3, 64),
-                                                   (X.MODE_STAGED, 2, 256), (X.MODE_LOWLAT, 1, 64)])
-def test_rx_pipe_end_to_end(mode, depth, step_batch):
-    """The pipelined loop (xsk_gpu_rx_pipe_*): up to `depth` batches in flight, one per context, completed in RX order;
-    every frame, verdict and counter exactly xsk_gpu_rx_step's (the oracle's), nothing left in flight after the flush."""
-    _dev()
-    holder = {}
-
-    def step(umem, rx, fq, tx, pool, n, totals):
-        if "p" not in holder:
-            holder["p"] = X.RxPipe(umem, 0, depth=depth, mode=mode)
-        got, res = holder["p"].step(rx, fq, tx, pool, n, totals)
-        assert holder["p"].inflight <= depth
-        return got, res
-
-    def flush(tx, pool, totals):
-        got, res = holder["p"].flush(tx, pool, totals)
-        assert holder["p"].inflight == 0
-        return got, res
-
-    try:
-        _drive(step, flush, step_batch, depth * step_batch)
-    finally:
-        if "p" in holder:
-            holder["p"].close()
-
-
-def test_rx_pipe_partial_timeouts():
-    """Every batch of a pipelined LOWLAT loop times out half served -- each context's resident grid is launched one
-    workgroup wide while its batches are posted for two (xsk_gpu__lowlat_test_width) -- and completes through the
-    launch path: still every frame exact, in order, and the contexts' outcome counters show the partial services."""
-    _dev()
-    holder = {}
-
-    def step(umem, rx, fq, tx, pool, n, totals):
-        if "p" not in holder:
-            p = holder["p"] = X.RxPipe(umem, 0, depth=2, mode=X.MODE_LOWLAT)
-            for i in range(2):
-                c = p.context(i)
-                if c.mode == X.MODE_LOWLAT:
-                    c.lowlat_tune(groups=2, timeout_us=3000)
-                    c.lowlat_test_width(1)
-        return holder["p"].step(rx, fq, tx, pool, n, totals)
-
-    try:
-        _drive(step, lambda tx, pool, totals: holder["p"].flush(tx, pool, totals), 64, 2 * 64, n_pkts=3000)
-        lowlat = [holder["p"].context(i) for i in range(2) if holder["p"].context(i).mode == X.MODE_LOWLAT]
-        assert lowlat, "no LOWLAT slot on this device"
-        for c in lowlat:
-            oc = c.lowlat_outcomes()
-            assert oc["partial"] > 0 and oc["untouched"] == 0, oc
-    finally:
-        if "p" in holder:
-            holder["p"].close()
