@@ -157,7 +157,7 @@ def test_tuning_code_is_not_in_the_product_library():
                                                     "xsk_gpu__staged_stats", "xsk_gpu__staged_noalias",
                                                     "xsk_gpu__multi_ctx", "xsk_gpu__lowlat_outcomes",
                                                     "xsk_gpu__lowlat_test_width", "xsk_gpu__rx_pipe_ctx",
-                                                    "xsk_gpu__lowlat_live"}, \
+                                                    "xsk_gpu__lowlat_live", "xsk_gpu__umem_view"}, \
         exported - set(declared_functions())
     tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
                           check=True).stdout

@@ -35,7 +35,7 @@ def run_batches(ctx, descs, batch, want_recs=True):
     return np.concatenate(vs), (np.concatenate(rs) if want_recs else None), tot
 
 
-def check(umem, work, descs, v, r, tot):
+def check(umem, work, descs, v, r, tot, ctx=None):
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
     assert (v == v_ref).all(), np.nonzero(v != v_ref)[0][:8]
@@ -45,10 +45,10 @@ def check(umem, work, descs, v, r, tot):
         assert tot[k] == int(s_ref[k]), k
     diff = np.nonzero(work != ref)[0]
     assert len(diff) == 0, f"{len(diff)} bytes differ, first at {diff[:8]}; " + describe_diff(umem, work, ref, descs, v,
-                                                                                               diff)
+                                                                                               diff, ctx)
 
 
-def describe_diff(umem, work, ref, descs, v, diff):
+def describe_diff(umem, work, ref, descs, v, diff, ctx=None):
     """Which frames' bytes differ, where, and whether they are still the request's (a write that never landed)."""
     addr = descs["addr"].astype(np.int64)
     out = []
@@ -56,9 +56,16 @@ def describe_diff(umem, work, ref, descs, v, diff):
         a = int(np.sort(addr)[j])
         i = int(np.nonzero(addr == a)[0][0])
         d = diff[(diff >= a) & (diff < a + 4096)] - a
+        gpu = ""
+        if ctx is not None and ctx.mode != X.MODE_STAGED:  # the same bytes through the GPU's translation
+            try:
+                g = ctx.umem_view(a, 64)
+                gpu = f" gpu-view {g[d[d < 64][:12]].tolist()} (matches host: {bool((g == work[a:a + 64]).all())})"
+            except Exception as e:  # noqa: BLE001 -- a report, not a check
+                gpu = f" gpu-view failed: {e}"
         out.append(f"frame {i} @{a} len {int(descs['len'][i])} verdict {int(v[i])}: offsets {d[:24].tolist()} "
                    f"got {work[a + d[:12]].tolist()} want {ref[a + d[:12]].tolist()} "
-                   f"request {umem[a + d[:12]].tolist()}")
+                   f"request {umem[a + d[:12]].tolist()}{gpu}")
     return " | ".join(out)
 
 
@@ -391,7 +398,7 @@ def test_lowlat_contexts_per_device_limit():
         assert 1 <= k <= X.LOWLAT_PER_DEVICE and modes == [X.MODE_LOWLAT] * k + [X.MODE_ZEROCOPY] * (len(modes) - k), modes
         for umem, descs, ctx in zip(umems, descss, ctxs):
             v, r, tot = run_batches(ctx, descs, 64)
-            check(umem, ctx.umem, descs, v, r, tot)
+            check(umem, ctx.umem, descs, v, r, tot, ctx)
             ref = umem.copy()
             oracle.echo_batch(ref, descs)
             assert (ctx.umem == ref).all()

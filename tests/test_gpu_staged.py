@@ -461,7 +461,7 @@ def test_lowlat_timeout_exactly_once():
                 outcomes.append(f"completed {ctx.lowlat_outcomes()}")
                 assert (v == v_ref).all() and (r == r_ref).all()
                 diff = np.nonzero(work != ref)[0]
-                assert len(diff) == 0, (rep, outcomes, describe_diff(umem, work, ref, descs, v, diff))
+                assert len(diff) == 0, (rep, outcomes, describe_diff(umem, work, ref, descs, v, diff, ctx))
                 assert int(st["tx_packets"]) == int(s_ref["tx_packets"])
             except X.XskGpuError as e:
                 assert e.rc == -errno.ETIMEDOUT, e
@@ -474,7 +474,7 @@ def test_lowlat_timeout_exactly_once():
                 v, r, _ = ctx.process(descs)  # the retry
                 assert (v == v_ref).all() and (r == r_ref).all()
                 diff = np.nonzero(work != ref)[0]
-                assert len(diff) == 0, (rep, outcomes, describe_diff(umem, work, ref, descs, v, diff))
+                assert len(diff) == 0, (rep, outcomes, describe_diff(umem, work, ref, descs, v, diff, ctx))
     print("timeout outcomes:", outcomes)
 
 
@@ -551,7 +551,7 @@ def test_lowlat_reserved_queue_for_an_application_stream():
             for umem, descs, ctx in zip(umems, descss, ctxs):
                 ctx.umem[:] = umem
                 v, r, tot = run_batches(ctx, descs, 64)
-                check(umem, ctx.umem, descs, v, r, tot)
+                check(umem, ctx.umem, descs, v, r, tot, ctx)
                 calls += len(descs) // 64
             if done_app is None and app.query():
                 done_app = time.perf_counter() - t0

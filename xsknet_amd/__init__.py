@@ -129,6 +129,7 @@ _SIGS = {
     "xsk_gpu__lowlat_test_width": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu__multi_ctx": ([_P, C.c_uint32], _P),
     "xsk_gpu__lowlat_live": ([C.c_int, C.POINTER(C.c_uint32)], C.c_int),
+    "xsk_gpu__umem_view": ([_P, C.c_uint64, _P, C.c_uint64], C.c_int),
     "xsk_gpu_rx_pipe_init": ([C.POINTER(_P), C.c_int, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
     "xsk_gpu_rx_pipe_step": ([_P, C.POINTER(Ring), C.POINTER(Ring), C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32,
                               _P, C.POINTER(RxResult)], C.c_int),
@@ -348,6 +349,12 @@ class EchoContext:
     def lowlat_test_width(self, wgs: int) -> None:
         """Test switch (xsk_gpu__lowlat_test_width): launch the resident grid with `wgs` workgroups (0 = all)."""
         _check("xsk_gpu__lowlat_test_width", lib().xsk_gpu__lowlat_test_width(self._ctx, wgs))
+
+    def umem_view(self, off: int, n: int) -> np.ndarray:
+        """xsk_gpu__umem_view: n bytes at `off` as the GPU's translation of the UMEM sees them (ZEROCOPY / LOWLAT)."""
+        out = np.zeros(n, np.uint8)
+        _check("xsk_gpu__umem_view", lib().xsk_gpu__umem_view(self._ctx, off, out.ctypes.data, n))
+        return out
 
     def lowlat_outcomes(self):
         """xsk_gpu__lowlat_outcomes: doorbell batches that missed their timeout -- all, completed through the launch

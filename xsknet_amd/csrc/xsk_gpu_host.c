@@ -343,6 +343,16 @@ int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[3]) {
     return 0;
 }
 xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
+int xsk_gpu__umem_view(xsk_gpu_ctx* c, uint64_t off, void* out, uint64_t n) {
+    if (!c || !out || !zerocopy(c) || off > c->umem_size || n > c->umem_size - off) return -EINVAL;
+    int rc = 0, caller_dev = -1;
+    if (hipGetDevice(&caller_dev) != hipSuccess) caller_dev = -1;
+    TRY(hipSetDevice(c->device));
+    TRY(hipMemcpy(out, c->d_umem + off, n, hipMemcpyDeviceToHost)); /* through the device alias's translation */
+out:
+    if (caller_dev >= 0 && caller_dev != c->device) (void)hipSetDevice(caller_dev);
+    return rc;
+}
 
 int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     if (!c || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;

@@ -231,6 +231,10 @@ int xsk_gpu__lowlat_test_width(xsk_gpu_ctx* ctx, uint32_t wgs);
  * `device` in this process right now (each adds itself when it starts and leaves when it exits): 0 once every LOWLAT
  * context is gone -- no grid outlives its channel. */
 int xsk_gpu__lowlat_live(int device, uint32_t* out);
+/* xsk_gpu_host.c (exported for the GPU tests' failure reports, not part of the ABI): n bytes of a ZEROCOPY / LOWLAT
+ * context's UMEM at `off`, copied through the context's device alias -- what the GPU's translation of those pages
+ * holds, to set beside the host's view of the same bytes. */
+int xsk_gpu__umem_view(xsk_gpu_ctx* ctx, uint64_t off, void* out, uint64_t n);
 
 #ifdef __cplusplus
 }
