@@ -390,15 +390,18 @@ uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_poo
  *
  * xsk_gpu_rx_pipe_step:
  *   1. if a context is free and the RX ring holds descriptors: peek up to min(max_batch, XSK_GPU_RX_MAX_STEP) of them,
- *      refill the fill ring (as xsk_gpu_rx_step), submit them and release the RX entries (the object keeps a copy of
- *      the descriptors: res->received);
+ *      submit them and release the RX entries (the object keeps a copy of the descriptors: res->received);
  *   2. complete batches in submission order -- the oldest when every context is busy, any that are already done, and
  *      all of them when step 1 found the RX ring empty -- each like xsk_gpu_rx_step's steps 4 and 5: replies onto the
- *      TX ring (or dropped and freed when it is full), every other frame back to `pool`, counters.
+ *      TX ring (or dropped and freed when it is full), every other frame back to `pool`, counters;
+ *   3. refill the fill ring from `pool` (as xsk_gpu_rx_step does, but on every call: frames freed by a step that
+ *      received nothing must reach the fill ring too, or with batches in flight it could run dry).
  * Returns the frames completed by this call (not the frames received), or a negative errno.  A batch whose completion
- * fails stays the oldest in flight and the error is returned; the next step or flush runs it again through its
- * context (as a caller retries a failed xsk_gpu_rx_step).  A failed submit leaves its frames on the RX ring.
- * xsk_gpu_rx_pipe_flush completes every batch in flight (an idle link, teardown).  xsk_gpu_rx_pipe_fini waits for
+ * fails stays the oldest in flight, and the next step or flush runs it again through its context (as a caller retries
+ * a failed xsk_gpu_rx_step); the call returns the error when it handed no frame on, else its count (the error comes
+ * back from a later call if the rerun fails too).  A failed submit leaves its frames on the RX ring.
+ * xsk_gpu_rx_pipe_flush completes every batch in flight (an idle link, teardown); with a failure it stops there, so
+ * call it until xsk_gpu_rx_pipe_inflight() is 0.  xsk_gpu_rx_pipe_fini waits for
  * batches still in flight and drops their results: flush first.  Single caller thread, like a context. */
 #define XSK_GPU_RX_PIPE_MAX 4u
 typedef struct xsk_gpu_rx_pipe xsk_gpu_rx_pipe;

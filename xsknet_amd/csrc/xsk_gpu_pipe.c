@@ -108,7 +108,6 @@ int xsk_gpu_rx_pipe_step(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* rx, struct xsk
         struct pipe_slot* s = &p->s[(p->head + p->count) % p->depth];
         uint32_t idx_rx = 0;
         const uint32_t rcvd = xr_cons_peek(rx, max_batch, &idx_rx); /* :196 */
-        r.refilled = xsk_gpu__rx_refill(fill, pool);                /* :201-217 */
         for (uint32_t i = 0; i < rcvd; i++) s->descs[i] = *xr_desc(rx, idx_rx + i);
         rc = xsk_gpu__submit(s->ctx, s->descs, rcvd, 0, 0);
         if (rc) { /* frames stay on the RX ring, as after a failed xsk_gpu_rx_step */
@@ -128,11 +127,18 @@ int xsk_gpu_rx_pipe_step(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* rx, struct xsk
         if (r.received && p->count < p->depth && (s->failed || !xsk_gpu__ready(s->ctx))) break;
         const int k = complete_oldest(p, tx, pool, stats, &r);
         if (k < 0) {
-            rc = k;
-            goto out;
+            /* the batch stays the oldest, to run again; frames this call already handed on are reported first (the
+             * error then comes from the next call if the rerun fails too) */
+            if (!done) rc = k;
+            break;
         }
         done += k;
     }
+    /* :201-217 -- the fill ring restocked on every step, after the completions: a batch completed by a step that
+     * received nothing (the ring ran empty) has freed its frames, and with several batches in flight they may be most
+     * of the UMEM; restocked only when frames arrive, as the reference does, the fill ring could run dry and no frame
+     * would arrive again */
+    r.refilled = xsk_gpu__rx_refill(fill, pool);
 out:
     if (res) *res = r;
     return rc ? rc : done;
@@ -146,7 +152,7 @@ int xsk_gpu_rx_pipe_flush(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* tx, struct xs
     while (p->count) {
         const int k = complete_oldest(p, tx, pool, stats, &r);
         if (k < 0) {
-            rc = k;
+            if (!done) rc = k; /* (as in a step: frames handed on are reported first) */
             break;
         }
         done += k;
