@@ -197,7 +197,7 @@ def test_multi_and_lowlat_validation_without_gpu():
     assert L.xsk_gpu_rx_pipe_inflight(None) == 0
     L.xsk_gpu_rx_pipe_fini(None)
     hdr = open(HEADER).read()
-    assert "XSK_GPU_RX_PIPE_MAX 4u" in hdr
+    assert f"XSK_GPU_RX_PIPE_MAX {X.RX_PIPE_MAX}u" in hdr
     assert "XSK_GPU_MODE_LOWLAT = 2" in hdr and f"XSK_GPU_LOWLAT_MAX {X.LOWLAT_MAX}u" in hdr
     assert f"XSK_GPU_MULTI_MAX {X.MULTI_MAX}" in hdr
 

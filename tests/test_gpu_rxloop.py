@@ -19,6 +19,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import xsknet_amd as X  # noqa: E402
+from tests.wire_frames import random_frame  # noqa: E402
 
 NUM_FRAMES, FRAME_SIZE, RING, HEADROOM = 4096, 4096, 2048, 256
 
@@ -55,10 +56,12 @@ def _dev():
         pytest.skip("no GPU")
 
 
-def _drive(step, flush, step_batch, cap, n_pkts=20000, seed=0x5EED0A0A):
+def _drive(step, flush, step_batch, cap, n_pkts=20000, seed=0x5EED0A0A, opts=0, wire=False):
     """Play the kernel side around `step(rx, fq, tx, pool, step_batch, totals) -> (frames completed, RxResult)` (and,
     for a pipelined loop, `flush(tx, pool, totals)` once the last packet is in): every transmitted reply and every
-    frame handed back is checked byte for byte against the oracle, in RX order, and the counters at the end."""
+    frame handed back is checked byte for byte against the oracle (with wire options `opts`), in RX order, and the
+    counters at the end.  wire: the packets are the wire generator's (VLAN stacks, IHL 3-15, fragments, padding, bad
+    checksums, tests/wire_frames.py) instead of the reference-mode generator's mixed traffic."""
     umem = np.zeros(NUM_FRAMES * FRAME_SIZE, np.uint8)
     rx, fq = KRing(X.DESC_DTYPE, False), KRing(np.uint64, True)
     tx, cq = KRing(X.DESC_DTYPE, True), KRing(np.uint64, False)
@@ -74,6 +77,7 @@ def _drive(step, flush, step_batch, cap, n_pkts=20000, seed=0x5EED0A0A):
     totals = np.zeros(1, X.STATS_DTYPE)
     ref_tot = {"rx_packets": 0, "rx_bytes": 0, "tx_packets": 0, "tx_bytes": 0}
     rng = np.random.default_rng(5)
+    rng_w = np.random.default_rng(seed ^ 0x77)
     sent = 0
     replies_seen = 0
     delivered = collections.deque()  # RX order
@@ -110,12 +114,19 @@ def _drive(step, flush, step_batch, cap, n_pkts=20000, seed=0x5EED0A0A):
             # aligned-chunk mode: the kernel masks a fill address to its chunk (the free stack
             # holds descriptor addresses, headroom included, as xsk_free_umem_frame stores them)
             a = (int(addr) & ~(FRAME_SIZE - 1)) + HEADROOM
-            L, buf = oracle.synth_frame(seed, sent, 1, 20, 1500, cap=FRAME_SIZE - HEADROOM)
+            if wire:
+                f, L = random_frame(rng_w, int(rng_w.choice([40, 200, 1400])))
+                buf = np.zeros(FRAME_SIZE - HEADROOM, np.uint8)
+                m = min(len(f), FRAME_SIZE - HEADROOM)
+                buf[:m] = np.frombuffer(f, np.uint8)[:m]
+                L = min(L, FRAME_SIZE - HEADROOM)
+            else:
+                L, buf = oracle.synth_frame(seed, sent, 1, 20, 1500, cap=FRAME_SIZE - HEADROOM)
             umem[a:a + FRAME_SIZE - HEADROOM] = buf[:FRAME_SIZE - HEADROOM]
             ref = buf[:FRAME_SIZE - HEADROOM].copy()
             d1 = np.zeros(1, oracle.DESC_DTYPE)
             d1[0] = (0, L, 0)
-            v, _, st = oracle.echo_batch(ref, d1)
+            v, _, st = oracle.echo_batch_opts(ref, d1, opts)
             for k in ref_tot:
                 ref_tot[k] += int(st[k])
             expect[a] = (sent, L, ref[:max(L, 64)].copy(), int(v[0]))

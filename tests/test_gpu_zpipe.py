@@ -9,7 +9,7 @@ illegal-address fault; the same sequence passed on the next boxes, the previous 
 and no leaked resident grid was ever found (the live-grid check after every test).  DESIGN.md §3.3 records the
 investigation.  Running these last keeps a repeat from reaching the rest of the suite.
 """
-import numpy as np  # noqa: F401
+import numpy as np
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -71,6 +71,31 @@ def test_rx_pipe_partial_timeouts():
         for c in lowlat:
             oc = c.lowlat_outcomes()
             assert oc["partial"] > 0 and oc["untouched"] == 0, oc
+    finally:
+        if "p" in holder:
+            holder["p"].close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_rx_pipe_randomised(seed):
+    """Random pipes: mode, depth, step size, wire options and traffic drawn per seed (fixed seeds), every frame exact."""
+    _dev()
+    rng = np.random.default_rng(0x5EEDB000 + seed)
+    mode = int(rng.choice([X.MODE_LOWLAT, X.MODE_LOWLAT, X.MODE_ZEROCOPY, X.MODE_STAGED]))
+    depth = int(rng.integers(1, X.RX_PIPE_MAX + 1))
+    step_batch = int(rng.choice([1, 7, 64, 200, 1024]))
+    wire = bool(rng.random() < 0.5)
+    opts = int(rng.choice([0, X.OPT_VLAN, X.OPT_STRICT_IPV4, X.OPT_VERIFY_CSUM, X.OPT_ALL])) if wire else 0
+    holder = {}
+
+    def step(umem, rx, fq, tx, pool, n, totals):
+        if "p" not in holder:
+            holder["p"] = X.RxPipe(umem, 0, depth=depth, mode=mode, opts=opts)
+        return holder["p"].step(rx, fq, tx, pool, n, totals)
+
+    try:
+        _drive(step, lambda tx, pool, totals: holder["p"].flush(tx, pool, totals), step_batch, depth * step_batch,
+               n_pkts=4000, seed=0x5EEDB100 + seed, opts=opts, wire=wire)
     finally:
         if "p" in holder:
             holder["p"].close()

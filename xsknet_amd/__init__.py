@@ -42,6 +42,7 @@ OPT_STRICT_IPV4, OPT_VLAN, OPT_VERIFY_CSUM, OPT_ALL = 1, 2, 4, 7
 F_IP_CSUM_OK, F_ICMP_CSUM_OK, F_VLAN, F_IP_OPTIONS = 1, 2, 4, 8
 MODE_ZEROCOPY, MODE_STAGED, MODE_LOWLAT = 0, 1, 2
 LOWLAT_MAX = 1024  # XSK_GPU_LOWLAT_MAX
+RX_PIPE_MAX = 4  # XSK_GPU_RX_PIPE_MAX
 MULTI_MAX = 16  # XSK_GPU_MULTI_MAX
 LOWLAT_PER_DEVICE = 4  # XSK_GPU_LOWLAT_PER_DEVICE
 
