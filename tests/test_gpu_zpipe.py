@@ -99,3 +99,28 @@ def test_rx_pipe_randomised(seed):
     finally:
         if "p" in holder:
             holder["p"].close()
+
+
+def test_rx_pipe_mixed_modes_when_slots_run_out():
+    """A LOWLAT pipe deeper than the device's free resident-kernel slots: with two of the four hardware queues reserved
+    for the application (xsk_gpu_lowlat_reserve), a 4-deep pipe runs two LOWLAT and two ZEROCOPY contexts side by side,
+    batches alternating between a doorbell and a launch -- still every frame exact, in order."""
+    _dev()
+    import gc
+    gc.collect()
+    cap = X.lowlat_reserve(0, 2)
+    holder = {}
+    try:
+        def step(umem, rx, fq, tx, pool, n, totals):
+            if "p" not in holder:
+                holder["p"] = X.RxPipe(umem, 0, depth=4, mode=X.MODE_LOWLAT)
+                modes = [holder["p"].context(i).mode for i in range(4)]
+                k = modes.count(X.MODE_LOWLAT)
+                assert k <= cap and modes == [X.MODE_LOWLAT] * k + [X.MODE_ZEROCOPY] * (4 - k), (cap, modes)
+            return holder["p"].step(rx, fq, tx, pool, n, totals)
+
+        _drive(step, lambda tx, pool, totals: holder["p"].flush(tx, pool, totals), 64, 4 * 64, n_pkts=8000)
+    finally:
+        if "p" in holder:
+            holder["p"].close()
+        X.lowlat_reserve(0, 0)
