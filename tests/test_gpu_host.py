@@ -428,3 +428,78 @@ def test_long_batch_split_launches_host_counters(mode):
     with X.EchoContext(work, 0, max_batch=n, mode=mode) as ctx:
         v, r, st = ctx.process(descs)
     check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
+
+
+def _small_frames_case(seed, n, wire):
+    """Small frames (<= 112 B) for the doorbell path: valid requests and every negative, unaligned starts,
+    frames at the UMEM's very end (window cut), descriptors past it (DROP_BAD_DESC), scrambled order."""
+    rng = np.random.default_rng(seed)
+    stride = 160
+    size = n * stride + 48
+    umem = rng.integers(0, 256, size, dtype=np.uint8)
+    tmp = np.zeros(n * 4096, np.uint8)
+    d = oracle.synth_batch(tmp, n, 0, 4096, seed=seed, mode=1, len_lo=20, len_hi=112, threads=4)
+    descs = np.zeros(n, X.DESC_DTYPE)
+    for j in range(n):
+        L = int(d["len"][j])
+        a = j * stride + int(rng.integers(0, 16))
+        if j == n - 1:
+            a = size - max(L, 38)  # the frame's end is the UMEM's end: its 64-B window is cut
+        umem[a:a + L] = tmp[j * 4096:j * 4096 + L]
+        descs[j] = (a, L, 0)
+    bad = rng.random(n) < 0.03
+    descs["addr"][bad] = size - 8
+    descs["len"][bad] = 100
+    if wire:
+        from tests.wire_frames import random_frame
+        for j in range(0, n, 3):
+            f, L = random_frame(rng, 40)
+            if L > 112 or len(f) > 112:
+                continue
+            a = int(descs["addr"][j])
+            if a + 112 > size or bad[j]:
+                continue
+            umem[a:a + len(f)] = np.frombuffer(f, np.uint8)
+            descs["len"][j] = L
+    return umem, np.ascontiguousarray(descs[rng.permutation(n)])
+
+
+@pytest.mark.parametrize("opts", [0, X.OPT_ALL])
+def test_lowlat_small_frames(opts):
+    """Doorbell batches of small frames (<= 112 B) at batch sizes 1-64: every byte, verdict, record and counter exactly
+    the oracle's, with unaligned frames, a frame whose 64-B window the UMEM's end cuts, and descriptors the transform
+    refuses."""
+    _dev()
+    umem, descs = _small_frames_case(0x5EEDD000 + opts, 900, opts != 0)
+    ref = umem.copy()
+    v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
+    for batch in (1, 5, 64):
+        work = umem.copy()
+        with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT, opts=opts) as ctx:
+            assert ctx.mode == X.MODE_LOWLAT
+            v, r, tot = run_batches(ctx, descs, batch)
+        assert (v == v_ref).all() and (r == r_ref).all(), batch
+        for k in COUNTERS:
+            assert tot[k] == int(s_ref[k]), (batch, k)
+        diff = np.nonzero(work != ref)[0]
+        assert len(diff) == 0, (batch, describe_diff(umem, work, ref, descs, v, diff))
+
+
+def test_lowlat_small_frames_partial_timeout():
+    """64-frame batches of small frames posted for two workgroups to a grid launched one workgroup wide: slice 0 is
+    served by the resident grid, slice 1 times out untouched and takes the launch path -- every call returns 0 and
+    every byte is the oracle's."""
+    _dev()
+    umem, descs = _small_frames_case(0x5EEDD100, 256, False)
+    ref = umem.copy()
+    v_ref, r_ref, _ = oracle.echo_batch(ref, descs)
+    work = umem.copy()
+    with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as ctx:
+        ctx.lowlat_tune(groups=2, timeout_us=5000)
+        ctx.lowlat_test_width(1)
+        v, r, _ = run_batches(ctx, descs, 64)
+        out = ctx.lowlat_outcomes()
+    assert out["partial"] == 4 and out["untouched"] == 0, out
+    assert (v == v_ref).all() and (r == r_ref).all()
+    diff = np.nonzero(work != ref)[0]
+    assert len(diff) == 0, describe_diff(umem, work, ref, descs, v, diff)
