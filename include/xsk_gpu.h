@@ -322,6 +322,16 @@ int xsk_gpu_classify_dev(const void* d_umem, uint64_t umem_size, const struct xs
                          int target_bound, uint8_t* d_actions, struct xsk_gpu_desc* d_out, uint32_t* d_nout,
                          void* d_workspace, void* stream);
 
+/* The UMEM allocation for the host modes: the reference allocates its UMEM with posix_memalign(getpagesize(),
+ * NUM_FRAMES * FRAME_SIZE) (src/lib/xsk_utils.c:132-135); this gives the same kind of memory (anonymous, private,
+ * page-aligned: AF_XDP registers it as it is) 2 MiB aligned, advised onto transparent huge pages and touched up front.
+ * The GPU then walks one translation per 2 MiB instead of one per 4 KiB frame chunk: a 64 x 64-B LOWLAT call 8.8 ->
+ * 7.2 us, a scattered 1024 x 64-B call 17.8 -> 12.9 (profiles/r05/hostlat_pages.jsonl).  size: a multiple of 16.
+ * *huge_bytes (may be NULL) = how much of it the kernel did back with huge pages (0 without THP).  0 or -errno.
+ * Release with xsk_gpu_umem_free(umem, size) after every context over it is gone. */
+int xsk_gpu_umem_alloc(void** umem, uint64_t size, uint64_t* huge_bytes);
+void xsk_gpu_umem_free(void* umem, uint64_t size);
+
 /* ------------------------------------------------------------------------------------------ */
 /* AF_XDP ring loop: the reference's handle_receive_packets() around one xsk_gpu_process().    */
 /* ------------------------------------------------------------------------------------------ */

@@ -266,3 +266,23 @@ def test_bench_kernel_names_are_the_shipped_kernels():
             short.add(m.group(1))
     assert bench.KERNEL in short, sorted(short)
     assert bench.WIRE_KERNEL in short, sorted(short)
+
+
+def test_umem_alloc_without_gpu():
+    """xsk_gpu_umem_alloc: 2 MiB aligned, zeroed, writable, argument checks (no device involved)."""
+    import xsknet_amd as X
+    L = X.lib()
+    p = C.c_void_p()
+    hb = C.c_uint64(0)
+    assert L.xsk_gpu_umem_alloc(C.byref(p), 0, None) == -errno.EINVAL
+    assert L.xsk_gpu_umem_alloc(C.byref(p), 4097, None) == -errno.EINVAL
+    assert L.xsk_gpu_umem_alloc(None, 4096, None) == -errno.EINVAL
+    with X.HugeUmem(5 << 20) as u:
+        assert u.array.ctypes.data % (2 << 20) == 0 and u.array.size == 5 << 20
+        assert not u.array.any()
+        u.array[::4096] = 7
+        assert int(u.array.sum()) == 7 * ((5 << 20) // 4096)
+        assert 0 <= u.huge_bytes <= 6 << 20
+    assert L.xsk_gpu_umem_alloc(C.byref(p), 16 << 20, C.byref(hb)) == 0 and p.value % (2 << 20) == 0
+    L.xsk_gpu_umem_free(p, 16 << 20)
+    L.xsk_gpu_umem_free(None, 0)

@@ -503,3 +503,20 @@ def test_lowlat_small_frames_partial_timeout():
     assert (v == v_ref).all() and (r == r_ref).all()
     diff = np.nonzero(work != ref)[0]
     assert len(diff) == 0, describe_diff(umem, work, ref, descs, v, diff)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c1_on_a_huge_page_umem(mode):
+    """BASELINE config 1 on a UMEM from xsk_gpu_umem_alloc (2 MiB aligned, transparent huge pages where the kernel
+    gives them): every mode exact, 64-frame batches, scrambled recycled order."""
+    _dev()
+    n = 4096
+    base = np.zeros(4096 * 4096, np.uint8)
+    descs = oracle.synth_batch(base, n, 256, 4096, seed=0x5EED0E0E, mode=1, len_lo=20, len_hi=1500)
+    descs = np.ascontiguousarray(descs[np.random.default_rng(3).permutation(n)])
+    with X.HugeUmem(base.size) as u:
+        u.array[:] = base
+        with X.EchoContext(u.array, 0, max_batch=64, mode=mode) as ctx:
+            v, r, tot = run_batches(ctx, descs, 64)
+        check(base, u.array, descs, v, r, tot)
+        print(f"huge-page bytes: {u.huge_bytes}")

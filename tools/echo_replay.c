@@ -71,6 +71,25 @@ static uint8_t* huge_copy(const uint8_t* src, size_t n) {
     return a;
 }
 
+/* AnonHugePages (KiB) of the mapping holding p (/proc/self/smaps): whether the kernel did back it with huge pages */
+static long huge_kb_at(const void* p) {
+    FILE* f = fopen("/proc/self/smaps", "r");
+    if (!f) return -1;
+    char line[512];
+    int in = 0;
+    long kb = -1;
+    while (fgets(line, sizeof line, f)) {
+        unsigned long lo = 0, hi = 0;
+        if (sscanf(line, "%lx-%lx ", &lo, &hi) == 2) {
+            in = (uintptr_t)p >= lo && (uintptr_t)p < hi;
+            continue;
+        }
+        if (in && sscanf(line, "AnonHugePages: %ld kB", &kb) == 1) break;
+    }
+    fclose(f);
+    return kb;
+}
+
 static int dump(const char* path, const void* p, size_t n) {
     FILE* f = fopen(path, "wb");
     if (!f) return -1;
@@ -215,6 +234,7 @@ int main(int argc, char** argv) {
            (unsigned long long)tx_ready);
     if (timed_calls) printf(" us_per_call=%.3f calls=%llu", timed_s / (double)timed_calls * 1e6,
                             (unsigned long long)timed_calls);
+    if (huge) printf(" huge_kb=%ld", huge_kb_at(umem));
     if (have_trace) {
         printf(" trace_ns=");
         for (int i = 0; i < 15; i++) printf("%s%llu", i ? "," : "", (unsigned long long)tr[i]);

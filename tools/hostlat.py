@@ -47,6 +47,8 @@ def run_one(exe, p, flen, mode, batch, tile, args):
     rec = {"frame_len": flen, "mode": mode, "batch": batch, "gpus": args.gpus or "0", "tile": tile or "auto", "groups": args.groups or "auto",
            "opts": args.opts, "umem_flushed": bool(args.flush), "umem_huge_pages": bool(args.huge), "scrambled": bool(args.scramble),
            "us_per_call": round(us, 2), "mframes_s": round(batch / us, 3), "calls": int(kv["calls"])}
+    if "huge_kb" in kv:  # the UMEM's AnonHugePages: whether the kernel backed it with 2 MiB pages
+        rec["umem_huge_kb"] = int(kv["huge_kb"])
     if "trace_ns" in kv:  # LOWLAT: the last batch's phases on the GPU
         t = [int(x) for x in kv["trace_ns"].split(",")]
         rec["last_batch_gpu_us"] = {

@@ -14,13 +14,14 @@
  *   - the application loop, on the queue's thread: xsk_gpu_tx_complete() (complete_tx minus the kick) and one
  *     xsk_gpu_rx_step() (or xsk_gpu_rx_pipe_step()) of up to <step> descriptors.  Throughput = frames / the loop's wall
  *     time (nic=thread) or / the summed step time (nic=inline).
+ * huge=1: the UMEM from xsk_gpu_umem_alloc (transparent huge pages) instead of posix_memalign's 4 KiB pages.
  * nic=burst measures the application and the GPU alone: untimed, the NIC fills the RX ring with every frame (ring =
  * frames); timed, the application's steps until each of them is completed (replies on the TX ring); repeat.  One NIC
  * thread that touches every frame caps nic=thread at a few tens of Mframes/s, below a pipelined loop.
  * A step takes min(ring occupancy, step, XSK_GPU_RX_MAX_STEP) frames; the reference's RX_BATCH_SIZE (64,
  * src/lib/xsk_utils.h:8) is a constant of its CPU loop and changes no frame's result.
  *
- *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0] [pipe=0] [nic=thread|inline|burst]
+ *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0] [pipe=0] [nic=thread|inline|burst] [huge=0]
  *
  * pipe=D (1..XSK_GPU_RX_PIPE_MAX): the pipelined loop instead -- xsk_gpu_rx_pipe_step() with up to D batches in flight
  * (one context each), a flush at the end; frames count when their batch completes.
@@ -116,7 +117,7 @@ static void ring_init(struct xsk_gpu_ring* r, struct ring_mem* m, uint32_t size,
 xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i); /* (library hook: a pipe's context) */
 
 struct queue {
-    uint32_t q, step, len, ring, frames, empty, pipe, nic_thread;
+    uint32_t q, step, len, ring, frames, empty, pipe, nic_thread, huge;
     int mode, real_mode;
     double seconds;
     /* results */
@@ -210,7 +211,8 @@ static void* run_queue(void* arg) {
     struct queue* Q = (struct queue*)arg;
     const uint32_t R = Q->ring, F = Q->frames, len = Q->len;
     uint8_t* umem = NULL;
-    if (posix_memalign((void**)&umem, 4096, (size_t)F * CHUNK)) {
+    if (Q->huge ? xsk_gpu_umem_alloc((void**)&umem, (uint64_t)F * CHUNK, NULL) != 0
+                : posix_memalign((void**)&umem, 4096, (size_t)F * CHUNK) != 0) {
         Q->rc = -12;
         return NULL;
     }
@@ -344,7 +346,8 @@ static void* run_queue(void* arg) {
     xsk_gpu_fini(ctx);
     if (st.rx_packets != Q->frames_done || st.tx_packets != Q->frames_done) Q->fail++;
     free(N.primed);
-    free(umem);
+    if (Q->huge) xsk_gpu_umem_free(umem, (uint64_t)F * CHUNK);
+    else free(umem);
     free(pool.addr);
     free(mrx.ents), free(mfill.ents), free(mtx.ents), free(mcomp.ents);
     return NULL;
@@ -360,7 +363,7 @@ int main(int argc, char** argv) {
     const int mode = !strcmp(argv[2], "lowlat") ? XSK_GPU_MODE_LOWLAT
                      : !strcmp(argv[2], "staged") ? XSK_GPU_MODE_STAGED : XSK_GPU_MODE_ZEROCOPY;
     const double seconds = atof(argv[3]);
-    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0, pipe = 0, nic = 1;
+    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0, pipe = 0, nic = 1, huge = 0;
     for (int a = 4; a < argc; a++) {
         if (!strncmp(argv[a], "len=", 4)) len = (uint32_t)atoi(argv[a] + 4);
         else if (!strncmp(argv[a], "queues=", 7)) nq = (uint32_t)atoi(argv[a] + 7);
@@ -368,6 +371,7 @@ int main(int argc, char** argv) {
         else if (!strncmp(argv[a], "frames=", 7)) frames = (uint32_t)atoi(argv[a] + 7);
         else if (!strncmp(argv[a], "empty=", 6)) empty = (uint32_t)atoi(argv[a] + 6);
         else if (!strncmp(argv[a], "pipe=", 5)) pipe = (uint32_t)atoi(argv[a] + 5);
+        else if (!strncmp(argv[a], "huge=", 5)) huge = (uint32_t)atoi(argv[a] + 5);
         else if (!strncmp(argv[a], "nic=", 4))
             nic = !strcmp(argv[a] + 4, "thread") ? 1u : !strcmp(argv[a] + 4, "burst") ? 2u : 0u;
     }
@@ -388,6 +392,7 @@ int main(int argc, char** argv) {
         Q[q].empty = empty;
         Q[q].pipe = pipe;
         Q[q].nic_thread = nic;
+        Q[q].huge = huge;
         Q[q].mode = mode;
         Q[q].seconds = seconds;
         pthread_create(&th[q], NULL, run_queue, &Q[q]);
@@ -396,8 +401,8 @@ int main(int argc, char** argv) {
     double t_max = 0.0;
     int rc = 0;
     printf("{\"tool\": \"rxring\", \"step\": %u, \"mode\": \"%s\", \"len\": %u, \"queues\": %u, \"ring\": %u, "
-           "\"frames\": %u, \"empty\": %u, \"pipe\": %u, \"timing\": \"%s\", \"per_queue\": [", step, argv[2], len, nq,
-           ring, frames, empty, pipe, nic == 2 ? "burst" : nic ? "wall" : "app");
+           "\"frames\": %u, \"empty\": %u, \"pipe\": %u, \"huge\": %u, \"timing\": \"%s\", \"per_queue\": [", step, argv[2],
+           len, nq, ring, frames, empty, pipe, huge, nic == 2 ? "burst" : nic ? "wall" : "app");
     for (uint32_t q = 0; q < nq; q++) {
         pthread_join(th[q], NULL);
         struct queue* R = &Q[q];

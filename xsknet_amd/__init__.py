@@ -131,6 +131,8 @@ _SIGS = {
     "xsk_gpu__multi_ctx": ([_P, C.c_uint32], _P),
     "xsk_gpu__lowlat_live": ([C.c_int, C.POINTER(C.c_uint32)], C.c_int),
     "xsk_gpu__umem_view": ([_P, C.c_uint64, _P, C.c_uint64], C.c_int),
+    "xsk_gpu_umem_alloc": ([C.POINTER(_P), C.c_uint64, C.POINTER(C.c_uint64)], C.c_int),
+    "xsk_gpu_umem_free": ([_P, C.c_uint64], None),
     "xsk_gpu_rx_pipe_init": ([C.POINTER(_P), C.c_int, _P, C.c_uint64, C.c_uint32, C.c_int], C.c_int),
     "xsk_gpu_rx_pipe_step": ([_P, C.POINTER(Ring), C.POINTER(Ring), C.POINTER(Ring), C.POINTER(FramePool), C.c_uint32,
                               _P, C.POINTER(RxResult)], C.c_int),
@@ -283,6 +285,31 @@ def lowlat_live(device: int = 0) -> int:
     out = C.c_uint32(0)
     _check("xsk_gpu__lowlat_live", lib().xsk_gpu__lowlat_live(device, C.byref(out)))
     return int(out.value)
+
+
+class HugeUmem:
+    """xsk_gpu_umem_alloc / xsk_gpu_umem_free: a UMEM on transparent huge pages (2 MiB aligned, touched up front);
+    `.array` is its numpy uint8 view, `.huge_bytes` how much of it the kernel backed with huge pages."""
+
+    def __init__(self, size: int):
+        self._p = C.c_void_p()
+        hb = C.c_uint64(0)
+        _check("xsk_gpu_umem_alloc", lib().xsk_gpu_umem_alloc(C.byref(self._p), size, C.byref(hb)))
+        self.size = size
+        self.huge_bytes = int(hb.value)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * size).from_address(self._p.value))
+
+    def close(self) -> None:
+        if self._p:
+            self.array = None
+            lib().xsk_gpu_umem_free(self._p, self.size)
+            self._p = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 STAGED_FIELDS = ("h2d_bytes", "strided", "span", "gather", "contained", "hostpack", "own_dma")

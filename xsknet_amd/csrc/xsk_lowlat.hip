@@ -412,8 +412,11 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     LL_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     LL_TRY(hipStreamCreateWithPriority(&ll->stream, hipStreamNonBlocking, hi));
     LL_TRY(hipHostMalloc((void**)&ll->h_bell, sizeof(xsk_gpu__bell), fl));
-    // XSK_GPU_LOWLAT_MAX slots plus a copy of the first 64 (the second poll's)
-    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc), dfl));
+    // XSK_GPU_LOWLAT_MAX slots plus a copy of the first 64 (the second poll's); fine-grained like the doorbell: every
+    // batch rewrites them, so no GPU cache should ever hold a copy (round 5: once in ~1 G frames a whole 256-frame slice
+    // came back DROP -- profiles/r05/rxpipe_pages.jsonl -- and a slice served from stale descriptors would do exactly
+    // that; not seen again in 0.9 G frames either way, profiles/r05/lowlat_slice_recheck.jsonl)
+    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc), fl));
     LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, dfl));
     LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), dfl));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
