@@ -1,6 +1,6 @@
 /*
- * xsk_gpu_umem.c — a UMEM allocation for the host modes: what the reference's xsk_configure_socket() gets from
- * posix_memalign(getpagesize(), NUM_FRAMES * FRAME_SIZE) (src/lib/xsk_utils.c:132-135), but 2 MiB aligned and
+ * xsk_gpu_umem.c — a UMEM allocation for the host modes: what the reference's init_xsk_socket() gets from
+ * posix_memalign(&buffer, getpagesize(), NUM_FRAMES * FRAME_SIZE) (src/lib/xsk_utils.c:132-135), but 2 MiB aligned and
  * advised onto transparent huge pages, and touched up front so the pages exist before the socket registers them.
  * The GPU reads a host-UMEM batch's frames through its own translations; on 4 KiB pages a 64-frame batch of frames one
  * per chunk walks 64 of them.  Measured through the resident kernel (tools/hostlat.py, profiles/r05/hostlat_pages.jsonl):
