@@ -124,3 +124,30 @@ def test_rx_pipe_mixed_modes_when_slots_run_out():
         if "p" in holder:
             holder["p"].close()
         X.lowlat_reserve(0, 0)
+
+
+@pytest.mark.parametrize("mode", [X.MODE_LOWLAT, X.MODE_ZEROCOPY])
+def test_rx_pipe_on_a_huge_page_umem(mode):
+    """The pipelined loop over a UMEM from xsk_gpu_umem_alloc (2 MiB aligned, transparent huge pages where the kernel
+    gives them; the registration then covers whole huge pages): depth 4, 64-frame steps, every frame exact."""
+    _dev()
+    holder = {}
+
+    def step(umem, rx, fq, tx, pool, n, totals):
+        if "p" not in holder:
+            holder["p"] = X.RxPipe(umem, 0, depth=4, mode=mode)
+        return holder["p"].step(rx, fq, tx, pool, n, totals)
+
+    def flush(tx, pool, totals):
+        got, res = holder["p"].flush(tx, pool, totals)
+        assert holder["p"].inflight == 0
+        return got, res
+
+    from tests.test_gpu_rxloop import FRAME_SIZE, NUM_FRAMES
+    with X.HugeUmem(NUM_FRAMES * FRAME_SIZE) as u:
+        try:
+            _drive(step, flush, 64, 4 * 64, umem=u.array)
+        finally:
+            if "p" in holder:
+                holder["p"].close()
+        print(f"huge-page bytes: {u.huge_bytes}")
