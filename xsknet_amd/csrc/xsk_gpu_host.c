@@ -166,8 +166,30 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
         }                                   \
     } while (0)
 
+/* the caller's current device, to put back on return: object lifecycles and per-call paths all select their own
+ * device and leave the caller's thread as they found it */
+int xsk_gpu__dev_save(void) {
+    int d = -1;
+    if (hipGetDevice(&d) != hipSuccess) {
+        (void)hipGetLastError();
+        d = -1;
+    }
+    return d;
+}
+void xsk_gpu__dev_restore(int d) {
+    int now = -1;
+    if (d >= 0 && (hipGetDevice(&now) != hipSuccess || now != d)) (void)hipSetDevice(d);
+}
+
+static void fini_impl(xsk_gpu_ctx* c);
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
     if (!c) return;
+    const int caller_dev = xsk_gpu__dev_save();
+    fini_impl(c);
+    xsk_gpu__dev_restore(caller_dev);
+}
+
+static void fini_impl(xsk_gpu_ctx* c) {
     (void)xsk_gpu__complete(c, NULL, NULL, NULL); /* a batch still in flight: let it finish (results dropped) */
     (void)hipSetDevice(c->device);
     xsk_gpu__lowlat_free(c->ll); /* stops the resident kernel (waits for it) ... */
@@ -308,19 +330,27 @@ out:
 }
 
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
-    return init_impl(out, device, umem, umem_size, max_batch, mode, 0);
+    const int caller_dev = xsk_gpu__dev_save();
+    const int rc = init_impl(out, device, umem, umem_size, max_batch, mode, 0);
+    xsk_gpu__dev_restore(caller_dev);
+    return rc;
 }
 
 int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
-    return init_impl(out, device, umem, umem_size, max_batch, mode, 1);
+    const int caller_dev = xsk_gpu__dev_save();
+    const int rc = init_impl(out, device, umem, umem_size, max_batch, mode, 1);
+    xsk_gpu__dev_restore(caller_dev);
+    return rc;
 }
 
 uint32_t xsk_gpu__ctx_max_batch(const xsk_gpu_ctx* c) { return c ? c->max_batch : 0u; }
 
 void xsk_gpu__ctx_quiesce(xsk_gpu_ctx* c) {
     if (!c || !c->ll || c->pend_n) return; /* (never with a batch in flight: its completion must see it served) */
+    const int caller_dev = xsk_gpu__dev_save();
     (void)hipSetDevice(c->device);
     xsk_gpu__lowlat_stop(c->ll);
+    xsk_gpu__dev_restore(caller_dev);
 }
 
 int xsk_gpu__staged_stats(const xsk_gpu_ctx* c, uint64_t out[XSK_GPU__STAGED_STATS]) {

@@ -236,6 +236,10 @@ int xsk_gpu__lowlat_live(int device, uint32_t* out);
  * holds, to set beside the host's view of the same bytes. */
 int xsk_gpu__umem_view(xsk_gpu_ctx* ctx, uint64_t off, void* out, uint64_t n);
 
+/* the caller's current device (-1 when unknown), and putting it back (xsk_gpu_host.c) */
+int xsk_gpu__dev_save(void);
+void xsk_gpu__dev_restore(int device);
+
 #ifdef __cplusplus
 }
 #endif

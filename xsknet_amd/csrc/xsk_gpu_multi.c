@@ -114,8 +114,10 @@ void xsk_gpu_multi_fini(xsk_gpu_multi* m) {
         free(w->recs);
     }
     if (m->registered) {
+        const int caller_dev = xsk_gpu__dev_save();
         (void)hipSetDevice(m->reg_device);
         (void)hipHostUnregister(m->umem);
+        xsk_gpu__dev_restore(caller_dev);
     }
     pthread_cond_destroy(&m->go);
     pthread_cond_destroy(&m->done);
@@ -146,8 +148,11 @@ int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, v
     int rc = 0;
     /* one registration of the caller's UMEM for every device (portable) with a device alias (mapped) */
     m->reg_device = devices[0];
-    if (hipSetDevice(devices[0]) != hipSuccess ||
-        hipHostRegister(umem, umem_size, hipHostRegisterPortable | hipHostRegisterMapped) != hipSuccess) {
+    const int caller_dev = xsk_gpu__dev_save();
+    const int reg = hipSetDevice(devices[0]) == hipSuccess &&
+                    hipHostRegister(umem, umem_size, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess;
+    xsk_gpu__dev_restore(caller_dev);
+    if (!reg) {
         rc = -EIO;
         goto fail;
     }
@@ -209,12 +214,8 @@ int xsk_gpu_multi_process(xsk_gpu_multi* m, const struct xsk_gpu_desc* descs, ui
     m->job_launch = !m->all_lowlat || (n + m->G - 1) / m->G > XSK_GPU_LOWLAT_MAX;
     /* (with a downgraded context no batch ever takes a doorbell, so no resident kernel is ever started: nothing to
      * stop, per call or otherwise -- ADVICE r04) */
-    if (m->job_launch && m->all_lowlat) {
-        int dev = -1;
-        const int have = hipGetDevice(&dev) == hipSuccess;
-        for (uint32_t g = 0; g < m->G; g++) xsk_gpu__ctx_quiesce(m->w[g].ctx);
-        if (have) (void)hipSetDevice(dev); /* the caller's current device, as it was */
-    }
+    if (m->job_launch && m->all_lowlat)
+        for (uint32_t g = 0; g < m->G; g++) xsk_gpu__ctx_quiesce(m->w[g].ctx); /* (each restores the caller's device) */
     if (m->G > 1) {
         pthread_mutex_lock(&m->mu);
         m->pending = m->G - 1;

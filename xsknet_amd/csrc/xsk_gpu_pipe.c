@@ -38,8 +38,10 @@ void xsk_gpu_rx_pipe_fini(xsk_gpu_rx_pipe* p) {
     if (!p) return;
     for (uint32_t i = 0; i < p->depth; i++) xsk_gpu_fini(p->s[i].ctx); /* (waits for a batch still in flight) */
     if (p->registered) {
+        const int caller_dev = xsk_gpu__dev_save();
         (void)hipSetDevice(p->device);
         (void)hipHostUnregister(p->umem);
+        xsk_gpu__dev_restore(caller_dev);
     }
     free(p);
 }
@@ -58,8 +60,11 @@ int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t
     p->umem = (uint8_t*)umem;
     int rc = 0;
     /* one registration of the UMEM, mapped, for every context of the pipe */
-    if (hipSetDevice(device) != hipSuccess || hipHostRegister(umem, umem_size, hipHostRegisterMapped) != hipSuccess) {
-        (void)hipGetLastError();
+    const int caller_dev = xsk_gpu__dev_save();
+    const int reg = hipSetDevice(device) == hipSuccess && hipHostRegister(umem, umem_size, hipHostRegisterMapped) == hipSuccess;
+    if (!reg) (void)hipGetLastError();
+    xsk_gpu__dev_restore(caller_dev);
+    if (!reg) {
         free(p);
         return -EIO;
     }
