@@ -29,6 +29,8 @@ hipError_t hipHostUnregister(void* p) {
     return hipSuccess;
 }
 hipError_t hipGetLastError(void) { return hipSuccess; }
+int xsk_gpu__dev_save(void) { return 0; }
+void xsk_gpu__dev_restore(int d) { (void)d; }
 
 /* ---- fake contexts ---- */
 #define NFRAMES 4096u

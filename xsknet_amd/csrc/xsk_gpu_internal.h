@@ -237,8 +237,8 @@ int xsk_gpu__lowlat_live(int device, uint32_t* out);
 int xsk_gpu__umem_view(xsk_gpu_ctx* ctx, uint64_t off, void* out, uint64_t n);
 
 /* the caller's current device (-1 when unknown), and putting it back (xsk_gpu_host.c) */
-int xsk_gpu__dev_save(void);
-void xsk_gpu__dev_restore(int device);
+__attribute__((visibility("hidden"))) int xsk_gpu__dev_save(void);
+__attribute__((visibility("hidden"))) void xsk_gpu__dev_restore(int device);
 
 #ifdef __cplusplus
 }
