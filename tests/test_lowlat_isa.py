@@ -147,3 +147,27 @@ def test_lowlat_completion_waits_for_the_write_back():
             m -= 1
             assert m > k - 256, (name, "no vector-memory op before the barrier")
         assert saw_wait, (name, "the wave's last vector-memory op is not waited for before the barrier", ins[m])
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM}/llvm-objdump"), reason="llvm-objdump not installed")
+def test_lowlat_reads_no_batch_data_through_the_scalar_cache():
+    """Each serving workgroup's acquire (`buffer_inv sc0 sc1`) invalidates the vector L1 and the L2's lines of host
+    memory, NOT the scalar data cache: a descriptor, frame or command word read with an `s_load` could come back from a
+    previous batch.  The resident kernel's scalar loads must be its kernel arguments (off the kernarg pointer s[0:1])
+    and the address of its live counter (a GOT entry: `s_getpc_b64` then the load) -- nothing else."""
+    funcs = lowlat_functions()
+    assert len(funcs) == 2, sorted(funcs)
+    for name, ins in funcs.items():
+        assert not any(s.startswith("s_dcache") for s in ins), name  # (and nothing that would need an invalidation)
+        for i, s in enumerate(ins):
+            if not (s.startswith("s_load") or s.startswith("s_buffer_load")):
+                continue
+            m = re.match(r"s_load_dword\w* s\[?[0-9:]+\]?, (s\[\d+:\d+\]), ", s)
+            assert m, (name, s)
+            if m.group(1) == "s[0:1]":
+                continue  # kernarg segment
+            base = m.group(1)
+            lo = base[2:].split(":")[0]
+            # the GOT entry: s_getpc_b64 base; s_add_u32 lo, lo, imm; s_addc_u32 hi, hi, 0; s_load base, base, 0x0
+            assert ins[i - 3] == f"s_getpc_b64 {base}" and ins[i - 2].startswith(f"s_add_u32 s{lo}, s{lo}, "), \
+                (name, ins[i - 4:i + 1])
