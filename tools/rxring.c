@@ -115,6 +115,7 @@ static void ring_init(struct xsk_gpu_ring* r, struct ring_mem* m, uint32_t size,
 }
 
 xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i); /* (library hook: a pipe's context) */
+int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[3]); /* (library hook: LOWLAT call outcomes) */
 
 struct queue {
     uint32_t q, step, len, ring, frames, empty, pipe, nic_thread, huge;
@@ -122,6 +123,8 @@ struct queue {
     double seconds;
     /* results */
     uint64_t frames_done, steps, checked, fail;
+    uint64_t dropped[3]; /* frames handed back without a reply: header still the request / the reply / other */
+    uint64_t outcomes[3]; /* LOWLAT batches past their timeout: all, completed partly served, failed (xsk_gpu__lowlat_outcomes) */
     double busy, wall;
     double* lat;
     uint64_t nlat;
@@ -141,6 +144,7 @@ struct nic {
     struct ring_mem *mrx, *mfill, *mtx, *mcomp;
     uint32_t R, len, k_rx_prod, k_fill_cons, k_tx_cons, k_comp_prod;
     uint8_t* primed; /* per chunk: the full request was written once (later only its header is restored) */
+    uint8_t* out;    /* per chunk: delivered on RX and not yet seen on TX */
     volatile int stop;
     uint64_t checked, fail;
 };
@@ -158,6 +162,7 @@ static void nic_pass(struct nic* N) {
     for (; N->k_tx_cons != tx_prod; N->k_tx_cons++) {
         const struct xsk_gpu_desc* d = &txe[N->k_tx_cons & (R - 1)];
         if (tx_prod - N->k_tx_cons > 16u) __builtin_prefetch(N->umem + txe[(N->k_tx_cons + 16u) & (R - 1)].addr);
+        N->out[d->addr / CHUNK] = 0;
         const uint64_t k = N->checked++;
         if (d->len != len) N->fail++;
         else if ((k & 3u) == 0 && memcmp(N->umem + d->addr, N->rep, (k & 63u) ? hdr : len) != 0) N->fail++;
@@ -180,6 +185,11 @@ static void nic_pass(struct nic* N) {
         const uint64_t base = ((uint64_t*)N->mfill->ents)[N->k_fill_cons & (R - 1)] & ~(uint64_t)(CHUNK - 1);
         const uint64_t c = base / CHUNK;
         uint8_t* f = N->umem + base + HEADROOM;
+        if (N->out[c]) { /* delivered, never transmitted, back on the fill ring: a frame the step did not answer */
+            const int is_req = !memcmp(f, N->req, hdr), is_rep = !memcmp(f, N->rep, hdr);
+            N->Q->dropped[is_req ? 0 : is_rep ? 1 : 2]++;
+        }
+        N->out[c] = 1;
         if (N->primed[c] && hdr == 64u) { /* 64-B aligned header, streamed */
             _mm_stream_si128((__m128i*)f, r0);
             _mm_stream_si128((__m128i*)f + 1, r1);
@@ -252,6 +262,7 @@ static void* run_queue(void* arg) {
     N.R = R;
     N.len = len;
     N.primed = (uint8_t*)calloc(F, 1);
+    N.out = (uint8_t*)calloc(F, 1);
     struct xsk_gpu_stats st;
     memset(&st, 0, sizeof st);
     const size_t cap = 1u << 22;
@@ -342,10 +353,16 @@ static void* run_queue(void* arg) {
     }
     Q->checked = N.checked;
     Q->fail += N.fail;
+    for (uint32_t i = 0; i < (pipe ? Q->pipe : 1u); i++) { /* LOWLAT outcomes, every context of the queue */
+        uint64_t o[3];
+        if (xsk_gpu__lowlat_outcomes(pipe ? xsk_gpu__rx_pipe_ctx(pipe, i) : ctx, o) == 0)
+            for (int k = 0; k < 3; k++) Q->outcomes[k] += o[k];
+    }
     if (pipe) xsk_gpu_rx_pipe_fini(pipe);
     xsk_gpu_fini(ctx);
     if (st.rx_packets != Q->frames_done || st.tx_packets != Q->frames_done) Q->fail++;
     free(N.primed);
+    free(N.out);
     if (Q->huge) xsk_gpu_umem_free(umem, (uint64_t)F * CHUNK);
     else free(umem);
     free(pool.addr);
@@ -411,10 +428,14 @@ int main(int argc, char** argv) {
         const double p50 = R->nlat ? R->lat[R->nlat / 2] : 0.0, p99 = R->nlat ? R->lat[(R->nlat * 99) / 100] : 0.0;
         const double T = nic ? R->wall : R->busy; /* the NIC in a thread of its own: the loop's wall time */
         printf("%s{\"mode\": %d, \"mframes_s\": %.3f, \"us_per_step\": %.3f, \"p50_us\": %.3f, \"p99_us\": %.3f, "
-               "\"frames_per_step\": %.1f, \"steps\": %llu, \"rc\": %d}", q ? ", " : "", R->real_mode,
+               "\"frames_per_step\": %.1f, \"steps\": %llu, \"dropped_req_rep_other\": [%llu, %llu, %llu], "
+               "\"lowlat_timeouts_all_partial_failed\": [%llu, %llu, %llu], \"rc\": %d}", q ? ", " : "", R->real_mode,
                T > 0 ? 1e-6 * (double)R->frames_done / T : 0.0, R->steps ? 1e6 * T / (double)R->steps : 0.0, 1e6 * p50,
                1e6 * p99,
-               R->steps ? (double)R->frames_done / (double)R->steps : 0.0, (unsigned long long)R->steps, R->rc);
+               R->steps ? (double)R->frames_done / (double)R->steps : 0.0, (unsigned long long)R->steps,
+               (unsigned long long)R->dropped[0], (unsigned long long)R->dropped[1], (unsigned long long)R->dropped[2],
+               (unsigned long long)R->outcomes[0], (unsigned long long)R->outcomes[1],
+               (unsigned long long)R->outcomes[2], R->rc);
         tot += R->frames_done;
         checked += R->checked;
         fail += R->fail;
