@@ -298,6 +298,30 @@ def host_inclusive(cfg, dev_index):
     return out
 
 
+def rx_loop(seconds=2.0):
+    """The AF_XDP RX loop per queue, measured by tools/rxring in a child process: one LOWLAT queue
+    against a simulated kernel side whose RX ring holds every frame of a burst (nic=burst: the application + GPU
+    alone), 64-B requests on a huge-page UMEM, every reply checked.  The reference's 64-frame step plain and pipelined
+    (xsk_gpu_rx_pipe_*, depth 4), and 1024-frame steps."""
+    exe = os.path.join(ROOT, "tools", "rxring")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/rxring not built (make)"}
+    out = {"tool": "tools/rxring", "timing": "burst", "frame_len": 64, "umem": "xsk_gpu_umem_alloc (huge pages)"}
+    for name, step, extra in (("step64", 64, []), ("step64_pipe4", 64, ["pipe=4"]), ("step1024", 1024, [])):
+        cmd = [exe, str(step), "lowlat", str(seconds), "len=64", "huge=1", "ring=16384", "frames=16384",
+               "nic=burst"] + extra
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=60 + 4 * seconds)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            q = d["per_queue"][0]
+            out[name] = {"mframes_per_s": q["mframes_s"], "us_per_step": q["us_per_step"], "p50_us": q["p50_us"],
+                         "p99_us": q["p99_us"], "frames": d["frames"], "checked": d["checked"],
+                         "failures": d["failures"], "mode": q["mode"]}
+        except Exception as e:  # a measurement leg: report, never fail the bench line
+            out[name] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
+    return out
+
+
 def multi_devices(world, share_gpu=False):
     """The GPUs of the multi-GPU host-inclusive leg: one context per rank's GPU (LOCAL_RANK r = cuda:r), or every
     context on cuda:0 in the one-GPU rehearsal."""
@@ -395,6 +419,7 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also measure the PCIe-inclusive rate")
+    ap.add_argument("--no-rx-loop", action="store_true", help="skip the RX-loop leg (tools/rxring, N = 1 only)")
     ap.add_argument("--no-host-multi", action="store_true",
                     help="N > 1: skip rank 0's multi-GPU host-inclusive leg after the timed region")
     ap.add_argument("--pool-cap", type=int, default=0, help="cap the batch pool (rehearsals on a shared GPU)")
@@ -592,6 +617,9 @@ def main():
         if world == 1 and not args.no_cpu:
             log("[rank 0] CPU baseline ...")
             res["cpu_baseline"] = cpu_baseline(args.config)
+        if world == 1 and not args.no_rx_loop:
+            log("[rank 0] RX loop (tools/rxring) ...")
+            res["rx_loop"] = rx_loop()
         if args.host_inclusive and world == 1:
             log("[rank 0] host-inclusive ...")
             res["host_inclusive"] = host_inclusive(args.config, local)

@@ -255,3 +255,22 @@ def test_host_inclusive_multi_devices_and_failure_is_recorded():
     out = bench.host_inclusive_multi("c3", 2, budget_s=0.05, n=256)
     assert out["devices"] == [0, 1] and out["frames_per_call"] == 256 and out["mode"] == "staged"
     assert "error" in out and "g2" not in out
+
+
+def test_rx_loop_leg_parses_rxring_and_never_fails_the_line(tmp_path, monkeypatch):
+    """bench.py's RX-loop leg: each tools/rxring run's JSON line becomes a record; a missing tool or a run that prints
+    no JSON is reported in the record, never raised (a measurement leg must not cost the bench line)."""
+    bench = _bench()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert "skipped" in bench.rx_loop(0.1)
+    (tmp_path / "tools").mkdir()
+    exe = tmp_path / "tools" / "rxring"
+    line = ('{"tool": "rxring", "per_queue": [{"mode": 2, "mframes_s": 28.7, "us_per_step": 4.2, "p50_us": 3.1, '
+            '"p99_us": 9.0}], "frames": 1000, "checked": 1000, "failures": 0, "rc": 0}')
+    exe.write_text("#!/bin/sh\ncase \"$*\" in *1024*) echo nothing; exit 1;; esac\necho '" + line + "'\n")
+    exe.chmod(0o755)
+    r = bench.rx_loop(0.1)
+    assert r["step64"] == {"mframes_per_s": 28.7, "us_per_step": 4.2, "p50_us": 3.1, "p99_us": 9.0, "frames": 1000,
+                           "checked": 1000, "failures": 0, "mode": 2}
+    assert r["step64_pipe4"]["mframes_per_s"] == 28.7
+    assert "error" in r["step1024"]
