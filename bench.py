@@ -302,21 +302,27 @@ def rx_loop(seconds=2.0):
     """The AF_XDP RX loop per queue, measured by tools/rxring in a child process: one LOWLAT queue
     against a simulated kernel side whose RX ring holds every frame of a burst (nic=burst: the application + GPU
     alone), 64-B requests on a huge-page UMEM, every reply checked.  The reference's 64-frame step plain and pipelined
-    (xsk_gpu_rx_pipe_*, depth 4), and 1024-frame steps."""
+    (xsk_gpu_rx_pipe_*, depth 4), 1024-frame steps, and the depth-8 pipe of a process started with
+    GPU_MAX_HW_QUEUES=8 (eight resident kernels: the deployment setting include/xsk_gpu.h names)."""
     exe = os.path.join(ROOT, "tools", "rxring")
     if not os.path.exists(exe):
         return {"skipped": "tools/rxring not built (make)"}
     out = {"tool": "tools/rxring", "timing": "burst", "frame_len": 64, "umem": "xsk_gpu_umem_alloc (huge pages)"}
-    for name, step, extra in (("step64", 64, []), ("step64_pipe4", 64, ["pipe=4"]), ("step1024", 1024, [])):
+    for name, step, extra, env in (("step64", 64, [], {}), ("step64_pipe4", 64, ["pipe=4"], {}),
+                                   ("step1024", 1024, [], {}),
+                                   ("step64_pipe8_hwq8", 64, ["pipe=8"], {"GPU_MAX_HW_QUEUES": "8"})):
         cmd = [exe, str(step), "lowlat", str(seconds), "len=64", "huge=1", "ring=16384", "frames=16384",
                "nic=burst"] + extra
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=60 + 4 * seconds)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=60 + 4 * seconds,
+                               env=dict(os.environ, **env))
             d = json.loads(r.stdout.strip().splitlines()[-1])
             q = d["per_queue"][0]
             out[name] = {"mframes_per_s": q["mframes_s"], "us_per_step": q["us_per_step"], "p50_us": q["p50_us"],
                          "p99_us": q["p99_us"], "frames": d["frames"], "checked": d["checked"],
                          "failures": d["failures"], "mode": q["mode"]}
+            if env:
+                out[name]["env"] = env
         except Exception as e:  # a measurement leg: report, never fail the bench line
             out[name] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     return out

@@ -208,8 +208,11 @@ enum xsk_gpu_mode {
  * The cap assumes the process runs NO other highest-priority streams on that device: an application stream of the
  * highest priority (hipStreamCreateWithPriority with the greatest priority, torch.cuda.Stream(priority=-1)) shares
  * those hardware queues, so its work may wait behind a resident kernel and a resident kernel behind its work.  An
- * application with such streams reserves one queue per stream first. */
-#define XSK_GPU_LOWLAT_PER_DEVICE 4
+ * application with such streams reserves one queue per stream first.
+ * With the runtime's default (GPU_MAX_HW_QUEUES unset or 4) that is 4; a deployment that sets GPU_MAX_HW_QUEUES=8 in
+ * its environment gets 8 (round 5, tools/rxring: a depth-8 pipelined RX loop at 64-frame steps 44-45 Mframes/s against
+ * 29-30 at depth 4). */
+#define XSK_GPU_LOWLAT_PER_DEVICE 8
 
 /* Reserve `queues` (<= XSK_GPU_LOWLAT_PER_DEVICE) of `device`'s highest-priority hardware queues for the application's
  * own highest-priority streams: LOWLAT contexts created afterwards stay within the rest (earlier ones keep running).
@@ -393,9 +396,12 @@ int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ri
 uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_pool* pool, uint32_t max);
 
 /* Pipelined RX loop: xsk_gpu_rx_step with up to `depth` batches in flight, so that one queue's steps overlap their
- * PCIe round trips instead of paying one per step.  The object owns `depth` contexts of `mode` over one registration
- * of the UMEM (LOWLAT contexts beyond the device's resident-kernel slots run as ZEROCOPY, as xsk_gpu_init does) and
- * hands batches to them in turn.  Frames of different batches are different frames, so batches in flight never
+ * PCIe round trips instead of paying one per step.  The object owns up to `depth` contexts of `mode` over one
+ * registration of the UMEM and hands batches to them in turn.  A LOWLAT pipe stops adding contexts at the first one
+ * the device has no resident-kernel slot left for (xsk_gpu_ctx_mode): batches complete in RX order, so one launched
+ * ZEROCOPY context among doorbell ones holds every batch behind it (4 LOWLAT + 4 ZEROCOPY at 64-frame steps: 5.2
+ * Mframes/s against 29 for the 4 LOWLAT alone); xsk_gpu_rx_pipe_depth() says how many it kept.  Only when not even the
+ * first context gets a slot are all `depth` contexts ZEROCOPY.  Frames of different batches are different frames, so batches in flight never
  * share a byte (the ownership contract above).
  *
  * xsk_gpu_rx_pipe_step:
@@ -413,7 +419,7 @@ uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_poo
  * xsk_gpu_rx_pipe_flush completes every batch in flight (an idle link, teardown); with a failure it stops there, so
  * call it until xsk_gpu_rx_pipe_inflight() is 0.  xsk_gpu_rx_pipe_fini waits for
  * batches still in flight and drops their results: flush first.  Single caller thread, like a context. */
-#define XSK_GPU_RX_PIPE_MAX 4u
+#define XSK_GPU_RX_PIPE_MAX 8u
 typedef struct xsk_gpu_rx_pipe xsk_gpu_rx_pipe;
 int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t umem_size, uint32_t depth, int mode);
 int xsk_gpu_rx_pipe_step(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* rx, struct xsk_gpu_ring* fill, struct xsk_gpu_ring* tx,
@@ -425,6 +431,8 @@ int xsk_gpu_rx_pipe_flush(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* tx, struct xs
 int xsk_gpu_rx_pipe_set_options(xsk_gpu_rx_pipe* p, uint32_t opts);
 /* Batches in flight now. */
 uint32_t xsk_gpu_rx_pipe_inflight(const xsk_gpu_rx_pipe* p);
+/* Contexts the pipe holds (its depth after init; at most the depth asked for).  0 for NULL. */
+uint32_t xsk_gpu_rx_pipe_depth(const xsk_gpu_rx_pipe* p);
 void xsk_gpu_rx_pipe_fini(xsk_gpu_rx_pipe* p);
 
 /* ------------------------------------------------------------------------------------------ */

@@ -44,11 +44,12 @@ static uint32_t rnd(uint32_t m) {
 
 struct xsk_gpu_ctx {
     uint32_t pend_n, countdown, max_batch, opts;
-    int fail_complete, fail_submit;
+    int fail_complete, fail_submit, mode;
     struct xsk_gpu_desc d[XSK_GPU_RX_MAX_STEP];
 };
 static struct xsk_gpu_ctx g_ctx[XSK_GPU_RX_PIPE_MAX];
 static uint32_t g_nctx;
+static int g_ll_left = 1000; /* the device's free resident-kernel slots (a LOWLAT request without one runs ZEROCOPY) */
 
 static uint8_t verdict_of(const struct xsk_gpu_desc* d) {
     if (d->len < 20u) return XSK_GPU_DROP_SHORT;
@@ -62,16 +63,25 @@ static void transform(const struct xsk_gpu_desc* d, uint32_t n, uint8_t* v) {
 }
 
 int xsk_gpu__init_prereg(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode) {
-    (void)device, (void)umem, (void)umem_size, (void)mode;
+    (void)device, (void)umem, (void)umem_size;
     struct xsk_gpu_ctx* c = &g_ctx[g_nctx++];
     memset(c, 0, sizeof *c);
     c->max_batch = max_batch;
+    c->mode = mode;
+    if (mode == XSK_GPU_MODE_LOWLAT) {
+        if (g_ll_left > 0) g_ll_left--;
+        else c->mode = XSK_GPU_MODE_ZEROCOPY;
+    }
     *out = c;
     return 0;
 }
 void xsk_gpu_fini(xsk_gpu_ctx* c) {
-    if (c) assert(c->pend_n == 0); /* the test flushes first */
+    if (!c) return;
+    assert(c->pend_n == 0); /* the test flushes first */
+    if (c->mode == XSK_GPU_MODE_LOWLAT) g_ll_left++;
+    c->mode = -1;
 }
+int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
 int xsk_gpu__submit(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n, int want_recs, int no_doorbell) {
     (void)want_recs, (void)no_doorbell;
     if (c->pend_n) return -EBUSY;
@@ -258,9 +268,36 @@ int main(void) {
         static uint8_t umem[64];
         xsk_gpu_rx_pipe* p = NULL;
         assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, 2, XSK_GPU_MODE_ZEROCOPY) == 0);
-        assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, 5, XSK_GPU_MODE_ZEROCOPY) == -EINVAL);
+        assert(xsk_gpu_rx_pipe_depth(p) == 2 && xsk_gpu_rx_pipe_depth(NULL) == 0);
+        xsk_gpu_rx_pipe_fini(p);
+        assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, XSK_GPU_RX_PIPE_MAX + 1, XSK_GPU_MODE_ZEROCOPY) == -EINVAL);
         assert(xsk_gpu_rx_pipe_init(&p, 1, umem, sizeof umem, 2, XSK_GPU_MODE_ZEROCOPY) == -ENODEV);
         xsk_gpu_rx_pipe_fini(p);
+    }
+    /* a LOWLAT pipe keeps doorbell contexts only: with 3 slots left a depth-8 request holds 3 LOWLAT contexts (the
+     * fourth, downgraded, is let go); with none, all 8 run ZEROCOPY; ZEROCOPY pipes are never trimmed */
+    {
+        static uint8_t umem[64];
+        for (int left = 0; left <= 9; left += 3) {
+            g_nctx = 0;
+            g_ll_left = left;
+            xsk_gpu_rx_pipe* p = NULL;
+            assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, 8, XSK_GPU_MODE_LOWLAT) == 0);
+            const uint32_t want = left == 0 ? 8u : (left < 8 ? (uint32_t)left : 8u);
+            assert(xsk_gpu_rx_pipe_depth(p) == want);
+            for (uint32_t i = 0; i < want; i++)
+                assert(xsk_gpu_ctx_mode(xsk_gpu__rx_pipe_ctx(p, i)) == (left ? XSK_GPU_MODE_LOWLAT : XSK_GPU_MODE_ZEROCOPY));
+            assert(g_ll_left == (left > 8 ? left - 8 : 0)); /* the let-go context held no slot */
+            xsk_gpu_rx_pipe_fini(p);
+            assert(g_ll_left == left);
+        }
+        g_nctx = 0;
+        g_ll_left = 1;
+        xsk_gpu_rx_pipe* p = NULL;
+        assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, 6, XSK_GPU_MODE_ZEROCOPY) == 0);
+        assert(xsk_gpu_rx_pipe_depth(p) == 6);
+        xsk_gpu_rx_pipe_fini(p);
+        g_ll_left = 1000;
     }
     printf("rx pipe ok\n");
     return 0;

@@ -187,7 +187,7 @@ def test_multi_and_lowlat_validation_without_gpu():
     L.xsk_gpu_multi_fini(None)
     # the pipelined RX loop: depth 1..XSK_GPU_RX_PIPE_MAX, a valid mode, an aligned UMEM; NULL objects
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 0, 2) == EINVAL
-    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 5, 2) == EINVAL
+    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, X.RX_PIPE_MAX + 1, 2) == EINVAL
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 2, 3) == EINVAL
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data + 1, 64, 2, 2) == EINVAL
     assert L.xsk_gpu_rx_pipe_init(None, 0, buf.ctypes.data, 64, 2, 2) == EINVAL

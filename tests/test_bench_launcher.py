@@ -274,3 +274,4 @@ def test_rx_loop_leg_parses_rxring_and_never_fails_the_line(tmp_path, monkeypatc
                            "checked": 1000, "failures": 0, "mode": 2}
     assert r["step64_pipe4"]["mframes_per_s"] == 28.7
     assert "error" in r["step1024"]
+    assert r["step64_pipe8_hwq8"]["env"] == {"GPU_MAX_HW_QUEUES": "8"}

@@ -459,7 +459,11 @@ def test_lowlat_timeout_exactly_once():
             try:
                 v, r, st = ctx.process(descs)
                 outcomes.append(f"completed {ctx.lowlat_outcomes()}")
-                assert (v == v_ref).all() and (r == r_ref).all()
+                bad = np.nonzero(r != r_ref)[0]
+                assert (v == v_ref).all() and len(bad) == 0, (
+                    rep, outcomes, f"{len(bad)} records differ, frames {bad[:8].tolist()}..{bad[-4:].tolist()}",
+                    [(f, r[bad[0]][f], r_ref[bad[0]][f]) for f in r.dtype.names if r[bad[0]][f] != r_ref[bad[0]][f]]
+                    if len(bad) else None, int((v != v_ref).sum()))
                 diff = np.nonzero(work != ref)[0]
                 assert len(diff) == 0, (rep, outcomes, describe_diff(umem, work, ref, descs, v, diff, ctx))
                 assert int(st["tx_packets"]) == int(s_ref["tx_packets"])

@@ -42,9 +42,9 @@ OPT_STRICT_IPV4, OPT_VLAN, OPT_VERIFY_CSUM, OPT_ALL = 1, 2, 4, 7
 F_IP_CSUM_OK, F_ICMP_CSUM_OK, F_VLAN, F_IP_OPTIONS = 1, 2, 4, 8
 MODE_ZEROCOPY, MODE_STAGED, MODE_LOWLAT = 0, 1, 2
 LOWLAT_MAX = 1024  # XSK_GPU_LOWLAT_MAX
-RX_PIPE_MAX = 4  # XSK_GPU_RX_PIPE_MAX
+RX_PIPE_MAX = 8  # XSK_GPU_RX_PIPE_MAX
 MULTI_MAX = 16  # XSK_GPU_MULTI_MAX
-LOWLAT_PER_DEVICE = 4  # XSK_GPU_LOWLAT_PER_DEVICE
+LOWLAT_PER_DEVICE = 8  # XSK_GPU_LOWLAT_PER_DEVICE (the cap is min(this, GPU_MAX_HW_QUEUES), 4 by default)
 
 # struct xsk_gpu_desc == struct xdp_desc (linux/if_xdp.h)
 DESC_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u4"), ("options", "<u4")])
@@ -139,6 +139,7 @@ _SIGS = {
     "xsk_gpu_rx_pipe_flush": ([_P, C.POINTER(Ring), C.POINTER(FramePool), _P, C.POINTER(RxResult)], C.c_int),
     "xsk_gpu_rx_pipe_set_options": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu_rx_pipe_inflight": ([_P], C.c_uint32),
+    "xsk_gpu_rx_pipe_depth": ([_P], C.c_uint32),
     "xsk_gpu_rx_pipe_fini": ([_P], None),
     "xsk_gpu__rx_pipe_ctx": ([_P, C.c_uint32], _P),
     # internal test / tool hook (xsk_gpu_internal.h): the product kernel with a forced workgroup count
@@ -507,7 +508,7 @@ class RxPipe:
     def __init__(self, umem: np.ndarray, device: int = 0, depth: int = 2, mode: int = MODE_LOWLAT, opts: int = 0):
         assert umem.dtype == np.uint8 and umem.flags.c_contiguous
         self.umem = umem
-        self.depth = depth
+        self.depth_asked = depth
         self._p = C.c_void_p()
         _check("xsk_gpu_rx_pipe_init", lib().xsk_gpu_rx_pipe_init(C.byref(self._p), device, umem.ctypes.data,
                                                                   umem.nbytes, depth, mode))
@@ -538,6 +539,11 @@ class RxPipe:
     @property
     def inflight(self) -> int:
         return int(lib().xsk_gpu_rx_pipe_inflight(self._p))
+
+    @property
+    def depth(self) -> int:
+        """Contexts the pipe holds: a LOWLAT pipe keeps doorbell contexts only (xsk_gpu_rx_pipe_depth)."""
+        return int(lib().xsk_gpu_rx_pipe_depth(self._p))
 
     def context(self, i: int) -> ContextView:
         """Context i of the pipe (xsk_gpu__rx_pipe_ctx): its mode, LOWLAT knobs and outcomes."""

@@ -107,11 +107,11 @@ static int hw_queues(void) {
     /* the HIP runtime's own variable (its hardware queues per process and priority; HIP's default is 4): not a
      * switch of this library */
     const char* e = getenv("GPU_MAX_HW_QUEUES");
-    q = XSK_GPU_LOWLAT_PER_DEVICE;
+    q = 4; /* unset: the runtime's default */
     if (e && *e) {
         char* end = NULL;
         const long v = strtol(e, &end, 10);
-        if (end != e && v >= 1 && v < q) q = (int)v;
+        if (end != e && v >= 1) q = v < XSK_GPU_LOWLAT_PER_DEVICE ? (int)v : XSK_GPU_LOWLAT_PER_DEVICE;
     }
     atomic_store(&g_hw_queues, q);
     return q;

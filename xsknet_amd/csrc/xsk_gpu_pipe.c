@@ -69,6 +69,7 @@ int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t
         return -EIO;
     }
     p->registered = 1;
+    uint32_t kept = depth;
     for (uint32_t i = 0; i < depth; i++) {
         rc = xsk_gpu__init_prereg(&p->s[i].ctx, device, umem, umem_size, XSK_GPU_RX_MAX_STEP, mode);
         if (rc) {
@@ -76,8 +77,17 @@ int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t
             xsk_gpu_rx_pipe_fini(p);
             return rc;
         }
+        /* a LOWLAT pipe keeps doorbell contexts only: completion is in RX order, so a launched (ZEROCOPY) context
+         * among them would hold every batch behind its own (include/xsk_gpu.h) */
+        if (i > 0 && mode == XSK_GPU_MODE_LOWLAT && xsk_gpu_ctx_mode(p->s[i].ctx) != XSK_GPU_MODE_LOWLAT &&
+            xsk_gpu_ctx_mode(p->s[0].ctx) == XSK_GPU_MODE_LOWLAT) {
+            xsk_gpu_fini(p->s[i].ctx);
+            p->s[i].ctx = NULL;
+            kept = i;
+            break;
+        }
     }
-    p->depth = depth;
+    p->depth = kept;
     *out = p;
     return 0;
 }
@@ -177,5 +187,7 @@ int xsk_gpu_rx_pipe_set_options(xsk_gpu_rx_pipe* p, uint32_t opts) {
 }
 
 uint32_t xsk_gpu_rx_pipe_inflight(const xsk_gpu_rx_pipe* p) { return p ? p->count : 0u; }
+
+uint32_t xsk_gpu_rx_pipe_depth(const xsk_gpu_rx_pipe* p) { return p ? p->depth : 0u; }
 
 xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i) { return p && i < p->depth ? p->s[i].ctx : NULL; }
