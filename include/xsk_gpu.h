@@ -211,7 +211,8 @@ enum xsk_gpu_mode {
  * application with such streams reserves one queue per stream first.
  * With the runtime's default (GPU_MAX_HW_QUEUES unset or 4) that is 4; a deployment that sets GPU_MAX_HW_QUEUES=8 in
  * its environment gets 8 (round 5, tools/rxring: a depth-8 pipelined RX loop at 64-frame steps 44-45 Mframes/s against
- * 29-30 at depth 4). */
+ * 29-30 at depth 4).  Not more: with 16 resident kernels the grids were time-sliced (a depth-16 pipe
+ * 0.12 Mframes/s), the device's hardware queue slots oversubscribed. */
 #define XSK_GPU_LOWLAT_PER_DEVICE 8
 
 /* Reserve `queues` (<= XSK_GPU_LOWLAT_PER_DEVICE) of `device`'s highest-priority hardware queues for the application's
