@@ -278,7 +278,7 @@ def host_inclusive(cfg, dev_index):
         devs = list(range(dev_index, dev_index + g)) if dev_index + g <= ndev else [dev_index] * g
         runs.append((f"staged_multi_g{g}", X.MODE_STAGED, devs))
     for name, mode, devs in runs:
-        work = umem.copy()
+        work = X.umem_copy(umem)  # page-aligned, as xsk_gpu_init requires
         mk = (lambda: X.EchoContext(work, dev_index, max_batch=n, mode=mode)) if devs is None else \
             (lambda: X.MultiContext(work, devs, max_batch=n, mode=mode))
         with mk() as ctx:
@@ -354,7 +354,7 @@ def host_inclusive_multi(cfg, world, budget_s=2.0, n=1 << 18):
         descs = oracle.synth_batch(umem, n, 0, stride, seed, mode=0, len_lo=lo, len_hi=hi, threads=cpu_share()[0])
         nbytes = int(descs["len"].sum())
         for g in sorted({1, len(devs)}):
-            work = umem.copy()
+            work = X.umem_copy(umem)  # page-aligned, as xsk_gpu_init requires
             with X.MultiContext(work, devs[:g], max_batch=n, mode=X.MODE_STAGED) as ctx:
                 v, _, _ = ctx.process(descs, want_recs=False)  # warm
                 ok = bool((v == X.TX_REPLY).all())

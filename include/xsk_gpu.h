@@ -16,7 +16,10 @@
  * prints and never exits (the reference logs and `exit()`s; per-frame failures are verdicts here).
  *
  * Frame ownership contract (AF_XDP gives every frame its own >= 2048-byte UMEM chunk):
- *   - the UMEM base is 16-byte aligned and the UMEM size is a multiple of 16;
+ *   - the UMEM size is a multiple of 16; a device UMEM's base is 16-byte aligned, a host UMEM's base
+ *     (xsk_gpu_init, xsk_gpu_multi_init, xsk_gpu_rx_pipe_init) page-aligned, as AF_XDP requires of the area
+ *     it registers (the reference: posix_memalign(getpagesize(), ...), src/lib/xsk_utils.c:132-135), so that
+ *     no page of a registered UMEM is shared with another allocation -- -EINVAL otherwise;
  *   - every frame exclusively owns the bytes [addr, addr + max(len, 64)) of the UMEM for the duration
  *     of a call (frames of one batch never overlap); the library only changes bytes
  *     [addr, addr + 38) of frames whose verdict is XSK_GPU_TX_REPLY (exactly the bytes the reference
@@ -222,8 +225,8 @@ enum xsk_gpu_mode {
 int xsk_gpu_lowlat_reserve(int device, uint32_t queues);
 
 /* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
- * xsk_utils.c:132-135).  The UMEM is page-locked (hipHostRegister) until xsk_gpu_fini().
- * max_batch bounds n of later calls. */
+ * xsk_utils.c:132-135; its base must be page-aligned, -EINVAL otherwise).  The UMEM is registered with the HIP
+ * runtime (hipHostRegister) until xsk_gpu_fini().  max_batch bounds n of later calls. */
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode);
 
 /* The mode `ctx` runs in (XSK_GPU_MODE_*): the one it was created with, except a LOWLAT request beyond

@@ -5,7 +5,10 @@
  * every frame transformed exactly once and handed on exactly once, in RX order (replies on the TX ring in RX order),
  * never more than `depth` batches in flight, a failed completion run again by the next step (its frames untouched
  * until then), a failed submit leaving its frames on the RX ring, the counters, and every frame accounted for at the
- * end.  Built and run by tests/test_rx_pipe.py. */
+ * end.  A failure whose batch may be partly transformed (a partly served doorbell batch whose launch path failed, a
+ * launch error: xsk_gpu__failed_untouched() == 0) drops the batch -- its frames back to the pool, none handed on, and
+ * no frame ever transformed twice (the pipe used to run such a batch again).
+ * Built and run by tests/test_rx_pipe.py. */
 #include <assert.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,6 +39,10 @@ void xsk_gpu__dev_restore(int d) { (void)d; }
 #define NFRAMES 4096u
 #define RING 1024u
 static uint32_t g_times[NFRAMES]; /* transformed, per frame */
+static uint32_t g_pos[NFRAMES];   /* fifo position of the frame's latest delivery */
+static uint8_t g_fifo_dropped[1u << 20], g_rep_dropped[1u << 20]; /* per delivery: its batch was dropped */
+static uint32_t g_rpos[NFRAMES];  /* rep_fifo position of its latest delivery (replies) */
+static uint64_t g_dropped, g_dropped_bytes, g_dropped_tx, g_dropped_tx_bytes, g_dropped_total;
 static uint64_t g_seed = 0x1234567u;
 static uint32_t rnd(uint32_t m) {
     g_seed = g_seed * 6364136223846793005ull + 1442695040888963407ull;
@@ -45,6 +52,7 @@ static uint32_t rnd(uint32_t m) {
 struct xsk_gpu_ctx {
     uint32_t pend_n, countdown, max_batch, opts;
     int fail_complete, fail_submit, mode;
+    int fail_partial, fail_submit_partial, untouched; /* unknown-outcome failures; the last failure's kind */
     struct xsk_gpu_desc d[XSK_GPU_RX_MAX_STEP];
 };
 static struct xsk_gpu_ctx g_ctx[XSK_GPU_RX_PIPE_MAX];
@@ -57,8 +65,26 @@ static uint8_t verdict_of(const struct xsk_gpu_desc* d) {
 }
 static void transform(const struct xsk_gpu_desc* d, uint32_t n, uint8_t* v) {
     for (uint32_t i = 0; i < n; i++) {
+        assert(g_times[d[i].addr / 4096u] == 0); /* never twice per delivery */
         g_times[d[i].addr / 4096u]++;
         if (v) v[i] = verdict_of(&d[i]);
+    }
+}
+
+/* the batch fails with part of it transformed: the pipe must drop it (frames back to the pool, none handed on) */
+static void fail_partly(const struct xsk_gpu_desc* d, uint32_t n) {
+    transform(d, (n + 1u) / 2u, NULL);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t f = (uint32_t)(d[i].addr / 4096u);
+        g_times[f] = 0;
+        g_fifo_dropped[g_pos[f]] = 1;
+        g_dropped++;
+        g_dropped_bytes += d[i].len;
+        if (verdict_of(&d[i]) == XSK_GPU_TX_REPLY) {
+            g_rep_dropped[g_rpos[f]] = 1;
+            g_dropped_tx++;
+            g_dropped_tx_bytes += d[i].len;
+        }
     }
 }
 
@@ -84,12 +110,19 @@ void xsk_gpu_fini(xsk_gpu_ctx* c) {
 int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
 int xsk_gpu__submit(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n, int want_recs, int no_doorbell) {
     (void)want_recs, (void)no_doorbell;
+    c->untouched = 1;
     if (c->pend_n) return -EBUSY;
     if (c->fail_submit) {
         c->fail_submit = 0;
         return -EIO;
     }
     assert(n >= 1 && n <= c->max_batch);
+    if (c->fail_submit_partial) { /* e.g. a launch error after the first chunks ran */
+        c->fail_submit_partial = 0;
+        c->untouched = 0;
+        fail_partly(d, n);
+        return -EIO;
+    }
     memcpy(c->d, d, n * sizeof *d);
     c->pend_n = n;
     c->countdown = rnd(4);
@@ -109,9 +142,16 @@ int xsk_gpu__complete(xsk_gpu_ctx* c, uint8_t* verdicts, struct xsk_gpu_rec* rec
     const uint32_t n = c->pend_n;
     if (!n) return 0;
     c->pend_n = 0;
+    c->untouched = 0;
     if (c->fail_complete) { /* timed out with every frame untouched */
         c->fail_complete = 0;
+        c->untouched = 1;
         return -ETIMEDOUT;
+    }
+    if (c->fail_partial) { /* part of the batch served, the rest's launch path failed */
+        c->fail_partial = 0;
+        fail_partly(c->d, n);
+        return -EIO;
     }
     transform(c->d, n, verdicts);
     return 0;
@@ -119,10 +159,12 @@ int xsk_gpu__complete(xsk_gpu_ctx* c, uint8_t* verdicts, struct xsk_gpu_rec* rec
 int xsk_gpu_process(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, uint32_t n, uint8_t* verdicts,
                     struct xsk_gpu_rec* recs, struct xsk_gpu_stats* stats) {
     (void)recs, (void)stats;
+    c->untouched = 1;
     if (c->pend_n) return -EBUSY;
     transform(d, n, verdicts);
     return 0;
 }
+int xsk_gpu__failed_untouched(const xsk_gpu_ctx* c) { return c->untouched; }
 int xsk_gpu_set_options(xsk_gpu_ctx* c, uint32_t opts) {
     c->opts = opts;
     return 0;
@@ -149,8 +191,11 @@ static void kring_init(struct kring* k, size_t esz, int app_produces) {
 
 static void run(uint32_t depth, uint32_t step, int faults) {
     memset(g_times, 0, sizeof g_times);
+    memset(g_fifo_dropped, 0, sizeof g_fifo_dropped);
+    memset(g_rep_dropped, 0, sizeof g_rep_dropped);
+    g_dropped = g_dropped_bytes = g_dropped_tx = g_dropped_tx_bytes = 0;
     g_nctx = 0;
-    static uint8_t umem[64];
+    static uint8_t umem[4096] __attribute__((aligned(4096)));
     xsk_gpu_rx_pipe* p = NULL;
     assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, depth, XSK_GPU_MODE_LOWLAT) == 0);
     struct kring rx, fq, tx, cq;
@@ -173,7 +218,7 @@ static void run(uint32_t depth, uint32_t step, int faults) {
     memset(&st, 0, sizeof st);
     uint64_t want_rx_bytes = 0, want_tx = 0, want_tx_bytes = 0;
     const uint64_t total = 60000;
-    for (uint32_t it = 0; handed < total; it++) {
+    for (uint32_t it = 0; handed + g_dropped < total; it++) {
         assert(it < 10000000u);
         /* kernel: deliver a burst (sometimes nothing, so the ring runs empty) */
         uint32_t burst = rnd(5) == 0 ? 0 : 1 + rnd(200);
@@ -187,9 +232,11 @@ static void run(uint32_t depth, uint32_t step, int faults) {
             if (verdict_of(d) == XSK_GPU_TX_REPLY) {
                 want_tx++;
                 want_tx_bytes += d->len;
+                g_rpos[a / 4096u] = r_tail;
                 rep_fifo[r_tail++] = a;
             }
             assert(g_times[a / 4096u] == 0); /* not transformed since it was last handed on */
+            g_pos[a / 4096u] = f_tail;
             fifo[f_tail++] = a;
             sent++;
             burst--;
@@ -197,18 +244,23 @@ static void run(uint32_t depth, uint32_t step, int faults) {
         /* faults: a completion that times out untouched, a submit that fails */
         if (faults && rnd(40) == 0) g_ctx[rnd(depth)].fail_complete = 1;
         if (faults && rnd(60) == 0) g_ctx[rnd(depth)].fail_submit = 1;
+        if (faults == 2 && rnd(50) == 0) g_ctx[rnd(depth)].fail_partial = 1;
+        if (faults == 2 && rnd(90) == 0) g_ctx[rnd(depth)].fail_submit_partial = 1;
         const uint32_t rx_cons0 = rx.cons, rx_prod0 = rx.prod;
+        const uint64_t dropped0 = g_dropped;
         struct xsk_gpu_rx_result res;
         const int got = xsk_gpu_rx_pipe_step(p, &rx.view, &fq.view, &tx.view, &pool, step, &st, &res);
         assert(xsk_gpu_rx_pipe_inflight(p) <= depth);
         if (got < 0) {
             assert(got == -ETIMEDOUT || got == -EIO);
-            if (got == -EIO) assert(rx.cons == rx_cons0 && rx.view.cached_cons == rx_cons0); /* frames stay on RX */
+            if (got == -EIO && g_dropped == dropped0) /* an untouched submit failure: the frames stay on RX */
+                assert(rx.cons == rx_cons0 && rx.view.cached_cons == rx_cons0);
             continue;
         }
         assert(res.received <= step && rx.cons - rx_cons0 == res.received && rx.prod == rx_prod0);
         /* every completed frame: transformed exactly once, handed on in RX order */
         for (int k = 0; k < got; k++) {
+            while (g_fifo_dropped[f_head]) f_head++; /* a dropped batch's frames are never handed on */
             const uint64_t a = fifo[f_head++];
             assert(g_times[a / 4096u] == 1);
             g_times[a / 4096u] = 0; /* (the frame may be delivered again once it is back on the fill ring) */
@@ -218,6 +270,7 @@ static void run(uint32_t depth, uint32_t step, int faults) {
         /* kernel: transmit in order, complete */
         while (tx.cons != tx.prod) {
             const struct xsk_gpu_desc* t = &((struct xsk_gpu_desc*)tx.ents)[tx.cons++ & (RING - 1)];
+            while (g_rep_dropped[r_head]) r_head++;
             assert(r_head < r_tail && t->addr == rep_fifo[r_head]);
             r_head++;
             replies++;
@@ -228,10 +281,11 @@ static void run(uint32_t depth, uint32_t step, int faults) {
             struct xsk_gpu_rx_result fr;
             int k = xsk_gpu_rx_pipe_flush(p, &tx.view, &pool, &st, &fr);
             if (k < 0) {
-                assert(k == -ETIMEDOUT);
+                assert(k == -ETIMEDOUT || k == -EIO);
                 k = 0;
             }
             for (int j = 0; j < k; j++) {
+                while (g_fifo_dropped[f_head]) f_head++;
                 const uint64_t a = fifo[f_head++];
                 assert(g_times[a / 4096u] == 1);
                 g_times[a / 4096u] = 0;
@@ -239,6 +293,7 @@ static void run(uint32_t depth, uint32_t step, int faults) {
             handed += (uint64_t)k;
             while (tx.cons != tx.prod) {
                 const struct xsk_gpu_desc* t = &((struct xsk_gpu_desc*)tx.ents)[tx.cons++ & (RING - 1)];
+                while (g_rep_dropped[r_head]) r_head++;
                 assert(t->addr == rep_fifo[r_head++]);
                 replies++;
                 ((uint64_t*)cq.ents)[cq.prod++ & (RING - 1)] = t->addr;
@@ -246,10 +301,15 @@ static void run(uint32_t depth, uint32_t step, int faults) {
             xsk_gpu_tx_complete(&cq.view, &pool, RING);
         }
     }
-    assert(handed == total && f_head == f_tail && r_head == r_tail && xsk_gpu_rx_pipe_inflight(p) == 0);
+    while (f_head < f_tail && g_fifo_dropped[f_head]) f_head++;
+    while (r_head < r_tail && g_rep_dropped[r_head]) r_head++;
+    assert(handed + g_dropped == total && f_head == f_tail && r_head == r_tail && xsk_gpu_rx_pipe_inflight(p) == 0);
+    if (faults < 2) assert(g_dropped == 0);
+    g_dropped_total += g_dropped;
     for (uint32_t f = 0; f < NFRAMES; f++) assert(g_times[f] == 0); /* nothing transformed and not handed on */
-    assert(st.rx_packets == total && st.rx_bytes == want_rx_bytes && st.tx_packets == want_tx &&
-           st.tx_bytes == want_tx_bytes && replies == want_tx);
+    assert(st.rx_packets == total - g_dropped && st.rx_bytes == want_rx_bytes - g_dropped_bytes &&
+           st.tx_packets == want_tx - g_dropped_tx && st.tx_bytes == want_tx_bytes - g_dropped_tx_bytes &&
+           replies == want_tx - g_dropped_tx);
     /* every frame accounted for: free stack + fill ring (nothing in flight, nothing on RX / TX / completion) */
     assert(pool.n_free + (fq.prod - fq.cons) == NFRAMES);
     assert(xsk_gpu_rx_pipe_set_options(p, XSK_GPU_OPT_ALL) == 0);
@@ -260,12 +320,13 @@ static void run(uint32_t depth, uint32_t step, int faults) {
 
 int main(void) {
     for (uint32_t depth = 1; depth <= XSK_GPU_RX_PIPE_MAX; depth++)
-        for (int faults = 0; faults < 2; faults++)
+        for (int faults = 0; faults < 3; faults++)
             for (uint32_t step = 1; step <= 1024; step *= 8) run(depth, step, faults);
+    assert(g_dropped_total > 0); /* the unknown-outcome failures did happen */
     /* argument checks */
     {
         g_nctx = 0;
-        static uint8_t umem[64];
+        static uint8_t umem[4096] __attribute__((aligned(4096)));
         xsk_gpu_rx_pipe* p = NULL;
         assert(xsk_gpu_rx_pipe_init(&p, 0, umem, sizeof umem, 2, XSK_GPU_MODE_ZEROCOPY) == 0);
         assert(xsk_gpu_rx_pipe_depth(p) == 2 && xsk_gpu_rx_pipe_depth(NULL) == 0);
@@ -277,7 +338,7 @@ int main(void) {
     /* a LOWLAT pipe keeps doorbell contexts only: with 3 slots left a depth-8 request holds 3 LOWLAT contexts (the
      * fourth, downgraded, is let go); with none, all 8 run ZEROCOPY; ZEROCOPY pipes are never trimmed */
     {
-        static uint8_t umem[64];
+        static uint8_t umem[4096] __attribute__((aligned(4096)));
         for (int left = 0; left <= 9; left += 3) {
             g_nctx = 0;
             g_ll_left = left;

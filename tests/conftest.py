@@ -12,13 +12,6 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
-    if os.environ.get("XSK_TEST_NO_THP") == "1":  # diagnosis only: no transparent huge pages in this process
-        import ctypes
-        ctypes.CDLL(None).prctl(41, 1, 0, 0, 0)  # PR_SET_THP_DISABLE
-    if os.environ.get("XSK_TEST_NO_NUMA_BALANCING") == "1":  # diagnosis only: a task policy without MPOL_F_MOF
-        import ctypes
-        mask = ctypes.c_ulong(1)  # node 0
-        ctypes.CDLL(None, use_errno=True).syscall(238, 1, ctypes.byref(mask), 64)  # set_mempolicy(MPOL_PREFERRED)
 
 
 @pytest.fixture(scope="session", autouse=True)

@@ -116,8 +116,11 @@ def test_abi_version_and_argument_validation():
     assert L.xsk_gpu_synth_dev(0x1000, 1 << 20, 0x2000, 4, 0, 2048, 0, 0, 1, 2, 64, 64, None) == EINVAL
     assert L.xsk_gpu_stream_read_dev(0x1000, 17, 0x2000, None) == EINVAL
     ctx = C.c_void_p()
-    buf = np.zeros(64, np.uint8)
+    import xsknet_amd as X
+    buf = X.umem_zeros(4096)
     assert L.xsk_gpu_init(C.byref(ctx), 0, None, 4096, 64, 0) == EINVAL
+    # a host UMEM starts on a page of its own (AF_XDP's rule, xsk_utils.c:132-135): 16-B alignment is not enough
+    assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data + 16, 64, 64, 0) == EINVAL
     assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data, 4095, 64, 0) == EINVAL
     assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data, 64, 0, 0) == EINVAL
     assert L.xsk_gpu_init(C.byref(ctx), 0, buf.ctypes.data, 64, 64, 7) == EINVAL
@@ -174,11 +177,12 @@ def test_multi_and_lowlat_validation_without_gpu():
     L = X.lib()
     EINVAL = -errno.EINVAL
     h = C.c_void_p()
-    buf = np.zeros(64, np.uint8)
+    buf = X.umem_zeros(4096)
     devs = (C.c_int * 1)(0)
     assert L.xsk_gpu_multi_init(C.byref(h), None, 1, buf.ctypes.data, 64, 64, 0) == EINVAL
     assert L.xsk_gpu_multi_init(C.byref(h), devs, 17, buf.ctypes.data, 64, 64, 0) == EINVAL
     assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data + 1, 64, 64, 0) == EINVAL
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data + 16, 64, 64, 0) == EINVAL
     assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data, 64, 0, 0) == EINVAL
     assert L.xsk_gpu_multi_init(C.byref(h), devs, 1, buf.ctypes.data, 64, 64, 3) == EINVAL
     assert L.xsk_gpu_init(C.byref(h), 0, buf.ctypes.data, 64, 64, 3) == EINVAL
@@ -190,6 +194,7 @@ def test_multi_and_lowlat_validation_without_gpu():
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, X.RX_PIPE_MAX + 1, 2) == EINVAL
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 2, 3) == EINVAL
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data + 1, 64, 2, 2) == EINVAL
+    assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data + 16, 64, 2, 2) == EINVAL
     assert L.xsk_gpu_rx_pipe_init(None, 0, buf.ctypes.data, 64, 2, 2) == EINVAL
     assert L.xsk_gpu_rx_pipe_step(None, None, None, None, None, 64, None, None) == EINVAL
     assert L.xsk_gpu_rx_pipe_flush(None, None, None, None, None) == EINVAL

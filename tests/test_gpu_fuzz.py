@@ -111,7 +111,7 @@ def test_fuzz_parity(seed):
         rng = np.random.default_rng(seed)
         mode = {"zerocopy": X.MODE_ZEROCOPY, "staged": X.MODE_STAGED, "staged_noalias": X.MODE_STAGED,
                 "lowlat": X.MODE_LOWLAT, "multi": int(rng.choice([X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT]))}[entry]
-        work = umem.copy()
+        work = X.umem_copy(umem)
         vs, rs, tot = [], [], {k: 0 for k in COUNTERS}
         mk = (lambda: X.MultiContext(work, [0] * int(rng.integers(2, 4)), max_batch=splits, mode=mode, opts=opts)) \
             if entry == "multi" else (lambda: X.EchoContext(work, 0, max_batch=splits, mode=mode, opts=opts))

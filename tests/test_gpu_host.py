@@ -77,7 +77,7 @@ def test_c1_exact_workload(mode):
     n = 4096
     umem = np.zeros(4096 * 4096, np.uint8)
     descs = oracle.synth_batch(umem, n, 256, 4096, seed=0x5EED0001, mode=0, len_lo=64, len_hi=64)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=64, mode=mode) as ctx:
         v, r, tot = run_batches(ctx, descs, 64)
     check(umem, work, descs, v, r, tot)
@@ -93,7 +93,7 @@ def test_lowlat_mixed_batches(batch):
     umem = np.zeros(n * 2048 + 4096, np.uint8)
     descs = oracle.synth_batch(umem, n, 256, 2048, seed=0x5EED1C1C + batch, mode=1, len_lo=20, len_hi=1900)
     for want in (True, False):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=max(batch, 1), mode=X.MODE_LOWLAT) as ctx:
             v, r, tot = run_batches(ctx, descs, batch, want_recs=want)
         check(umem, work, descs, v, r, tot)
@@ -113,7 +113,7 @@ def test_lowlat_completion_never_overtakes_outputs():
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
     assert (v_ref[0::2] == X.TX_REPLY).all() and (v_ref[1::2] != X.TX_REPLY).all()
     for batch in (1, 3):  # odd: consecutive calls' verdict patterns differ
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_LOWLAT) as ctx:
             v, r, tot = run_batches(ctx, descs, batch)
         check(umem, work, descs, v, r, tot)
@@ -127,7 +127,7 @@ def test_lowlat_idle_exit_large_batches_and_options():
     n = 3 * 1024 + 2048 + 512
     umem = np.zeros(n * 2048, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED1D1D, mode=1, len_lo=20, len_hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     parts = [(0, 64), (64, 1024), (1088, 2048), (3136, 1000), (4136, 512), (4648, n - 4648)]
     tot = {k: 0 for k in COUNTERS}
     vs = []
@@ -141,7 +141,7 @@ def test_lowlat_idle_exit_large_batches_and_options():
                 tot[k] += int(s[k])
     check(umem, work, descs, np.concatenate(vs), None, tot)
     # wire mode through the doorbell (the spec oracle: oracle_echo_batch_opts)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
         v0, _, _ = ctx.process(descs[:64], want_recs=False)
         ctx.set_options(X.OPT_ALL)
@@ -162,7 +162,7 @@ def test_lowlat_many_small_calls():
     descs = oracle.synth_batch(umem, n, 256, 4096, seed=0x5EED1E1E, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     t = 0.0
     with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_LOWLAT) as ctx:
         for p in range(passes):
@@ -187,7 +187,7 @@ def test_multi_context_one_gpu(mode, devices):
     umem = np.zeros(n * 2048 + 256, np.uint8)
     descs = oracle.synth_batch(umem, n, 256, 2048, seed=0x5EED2020 + len(devices), mode=1, len_lo=20, len_hi=1500)
     for batch in (64, 3001, n):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.MultiContext(work, devices, max_batch=batch, mode=mode) as m:
             v, r, tot = run_batches(m, descs, batch)
         check(umem, work, descs, v, r, tot)
@@ -198,7 +198,7 @@ def test_multi_context_wire_options():
     n = 4000
     umem = np.zeros(n * 2048, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2121, mode=1, len_lo=20, len_hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.MultiContext(work, [0, 0], max_batch=n, mode=X.MODE_STAGED, opts=X.OPT_ALL) as m:
         v, r, _ = m.process(descs)
     ref = umem.copy()
@@ -210,9 +210,11 @@ def test_multi_context_argument_checks():
     import ctypes as C
     import errno
     L = X.lib()
-    buf = np.zeros(4096, np.uint8)
+    buf = X.umem_zeros(4096)
     h = C.c_void_p()
     devs = (C.c_int * 2)(0, 0)
+    # a host UMEM starts on a page of its own (include/xsk_gpu.h; AF_XDP's rule)
+    assert L.xsk_gpu_multi_init(C.byref(h), devs, 2, buf.ctypes.data + 16, buf.nbytes - 16, 64, 0) == -errno.EINVAL
     assert L.xsk_gpu_multi_init(C.byref(h), devs, 0, buf.ctypes.data, buf.nbytes, 64, 0) == -errno.EINVAL
     assert L.xsk_gpu_multi_init(C.byref(h), devs, 2, buf.ctypes.data, buf.nbytes, 64, 9) == -errno.EINVAL
     bad = (C.c_int * 2)(0, 999)
@@ -232,7 +234,7 @@ def test_lowlat_posts_near_idle_exit(batch):
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2323, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     rng = np.random.default_rng(11)
     tot = {k: 0 for k in COUNTERS}
     with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_LOWLAT) as ctx:
@@ -261,7 +263,7 @@ def test_lowlat_workgroup_slices(groups, flen):
     mode = 0 if flen == 1500 else 1
     descs = oracle.synth_batch(umem, n, 256, 2048, seed=0x5EED2424 + groups + flen, mode=mode, len_lo=20 if mode else flen,
                                len_hi=flen)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     tot = {k: 0 for k in COUNTERS}
     vs, rs = [], []
     with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
@@ -289,7 +291,7 @@ def test_lowlat_timeout_quiesces_and_recovers():
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2525, mode=0, len_lo=1500, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, _ = oracle.echo_batch(ref, descs)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     timed_out = 0
     with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
         ctx.process(descs[1024:1025])  # the grid is up
@@ -327,7 +329,7 @@ def test_multi_context_partial_failure():
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
     for mode in (X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT):
         for batch in (300, n):  # doorbell-sized shares (LOWLAT) and launched ones
-            work = umem.copy()
+            work = X.umem_copy(umem)
             with X.MultiContext(work, [0, 0, 0], max_batch=batch, mode=mode) as m:
                 m.inject_failure(1, -errno.EIO)
                 d = np.ascontiguousarray(descs[:batch])
@@ -363,7 +365,7 @@ def test_multi_lowlat_path_chosen_per_batch():
     n = 2049 + 128 + 2049
     umem = np.zeros(n * 2048, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED2727, mode=1, len_lo=20, len_hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     tot = {k: 0 for k in COUNTERS}
     vs = []
     with X.MultiContext(work, [0, 0], max_batch=2049, mode=X.MODE_LOWLAT) as m:
@@ -391,7 +393,7 @@ def test_lowlat_contexts_per_device_limit():
             descs = oracle.synth_batch(umem, n, 256, 4096, 0x5EED4040 + q, mode=1, len_lo=20, len_hi=1500)
             umems.append(umem)
             descss.append(descs)
-            ctxs.append(X.EchoContext(umem.copy(), 0, max_batch=64, mode=X.MODE_LOWLAT))
+            ctxs.append(X.EchoContext(X.umem_copy(umem), 0, max_batch=64, mode=X.MODE_LOWLAT))
         modes = [c.mode for c in ctxs]
         # LOWLAT while a slot is free, ZEROCOPY from then on (a context another test still holds takes a slot too)
         k = modes.count(X.MODE_LOWLAT)
@@ -405,7 +407,7 @@ def test_lowlat_contexts_per_device_limit():
     finally:
         for c in ctxs:
             c.close()
-    again = [X.EchoContext(np.zeros(1 << 16, np.uint8), 0, max_batch=64, mode=X.MODE_LOWLAT) for _ in range(k)]
+    again = [X.EchoContext(X.umem_zeros(1 << 16), 0, max_batch=64, mode=X.MODE_LOWLAT) for _ in range(k)]
     try:
         assert [c.mode for c in again] == [X.MODE_LOWLAT] * k  # fini gave the slots back
     finally:
@@ -424,7 +426,7 @@ def test_long_batch_split_launches_host_counters(mode):
     umem = np.zeros(n * 64, np.uint8)
     descs = oracle.synth_batch(umem, n, 0, 64, 0x5EED5252, mode=1, len_lo=20, len_hi=64,
                                threads=min(16, oracle.cpu_threads()))
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=n, mode=mode) as ctx:
         v, r, st = ctx.process(descs)
     check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
@@ -474,7 +476,7 @@ def test_lowlat_small_frames(opts):
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, opts)
     for batch in (1, 5, 64):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT, opts=opts) as ctx:
             assert ctx.mode == X.MODE_LOWLAT
             v, r, tot = run_batches(ctx, descs, batch)
@@ -493,7 +495,7 @@ def test_lowlat_small_frames_partial_timeout():
     umem, descs = _small_frames_case(0x5EEDD100, 256, False)
     ref = umem.copy()
     v_ref, r_ref, _ = oracle.echo_batch(ref, descs)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as ctx:
         ctx.lowlat_tune(groups=2, timeout_us=5000)
         ctx.lowlat_test_width(1)

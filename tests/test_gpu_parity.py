@@ -277,7 +277,7 @@ def test_host_umem_modes(mode):
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
     for batch in (64, 4096):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=batch, mode=mode) as ctx:
             tot = {k: 0 for k in ("rx_packets", "rx_bytes", "tx_packets", "tx_bytes")}
             vs, rs = [], []
@@ -538,7 +538,7 @@ def test_staged_pipeline_multi_chunk():
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED0909, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
         v, r, s = ctx.process(descs)
     assert (v == v_ref).all()

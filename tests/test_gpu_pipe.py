@@ -2,12 +2,10 @@
 tests/test_gpu_rxloop.py (whose driver, `_drive`, plays it): up to `depth` batches in flight, one per context over one
 registration of the UMEM, completed in RX order, every frame, verdict and counter exactly the oracle's.
 
-These tests sit in a file of their own that sorts after every other GPU test file.  In round 5, on some MI355X boxes
-and not others, tests that ran later in the same process than these (LOWLAT timeouts, multi objects, STAGED copy-ins --
-paths these tests do not change) saw GPU writes to host-registered UMEM pages land a few pages away, and once an
-illegal-address fault; the same sequence passed on the next boxes, the previous commit never met such a box in an A/B,
-and no leaked resident grid was ever found (the live-grid check after every test).  DESIGN.md §3.3 records the
-investigation.  Running these last keeps a repeat from reaching the rest of the suite.
+Round 5 ran these last (the file was test_gpu_zpipe.py) after tests that ran later in the same process had seen
+replies land a few pages away from their host frames on some boxes; round 6 put them back in collection order once the
+host UMEMs of every test were page-aligned (xsk_gpu_init now requires it, as AF_XDP does) -- DESIGN.md §4 has the
+investigation and what it did and did not establish.
 """
 import numpy as np
 import pytest

@@ -62,9 +62,9 @@ def _drive(step, flush, step_batch, cap, n_pkts=20000, seed=0x5EED0A0A, opts=0, 
     frame handed back is checked byte for byte against the oracle (with wire options `opts`), in RX order, and the
     counters at the end.  wire: the packets are the wire generator's (VLAN stacks, IHL 3-15, fragments, padding, bad
     checksums, tests/wire_frames.py) instead of the reference-mode generator's mixed traffic.  umem: a caller-owned
-    zeroed uint8 array of NUM_FRAMES * FRAME_SIZE bytes (e.g. X.HugeUmem's) instead of a fresh numpy one."""
+    zeroed uint8 array of NUM_FRAMES * FRAME_SIZE bytes (e.g. X.HugeUmem's) instead of a fresh page-aligned one."""
     if umem is None:
-        umem = np.zeros(NUM_FRAMES * FRAME_SIZE, np.uint8)
+        umem = X.umem_zeros(NUM_FRAMES * FRAME_SIZE)
     assert umem.dtype == np.uint8 and umem.size == NUM_FRAMES * FRAME_SIZE
     rx, fq = KRing(X.DESC_DTYPE, False), KRing(np.uint64, True)
     tx, cq = KRing(X.DESC_DTYPE, True), KRing(np.uint64, False)

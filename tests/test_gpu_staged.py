@@ -62,7 +62,7 @@ def test_staged_scrambled_multi_chunk():
     _dev()
     n = 3 * CHUNK + 777
     umem, descs = scrambled(n, n + n // 4, 2048, 0, 0x5EED4A4A, mode=1, lo=20, hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
         v, r, st = ctx.process(descs)
         rec = ctx.staged_stats()
@@ -95,7 +95,7 @@ def test_staged_strided_multi_chunk_back_to_back():
         else:
             assert not any(p[1] for p in plans if p[0] == SP.TWO_D)
         for rep in range(3 if mode == 0 else 1):
-            work = umem.copy()
+            work = X.umem_copy(umem)
             with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
                 v, r, st = ctx.process(descs)
                 rec = ctx.staged_stats()
@@ -135,7 +135,7 @@ def test_staged_multi_chunk_overlapping_spans():
     order = np.concatenate([np.arange(c, n, 3) for c in range(3)])
     descs = np.ascontiguousarray(descs[order])
     for rep in range(3):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
             v, r, st = ctx.process(descs)
             rec = ctx.staged_stats()
@@ -160,14 +160,14 @@ def test_staged_copy_in_paths():
     u = np.zeros(n * 2048, np.uint8)
     cases.append(("gather", u, oracle.synth_batch(u, n, 0, 2048, 0x5EED4C03, mode=0, len_lo=64, len_hi=1500)))
     for path, umem, descs in cases:
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
             v, r, st = ctx.process(descs)
             rec = ctx.staged_stats()
         check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
         assert rec[path] == 1 and sum(rec[k] for k in ("strided", "span", "gather")) == 1, (path, rec)
         assert rec["h2d_bytes"] <= 1.1 * owned_bytes(descs), (path, rec, owned_bytes(descs))
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_STAGED) as ctx:
             v, r, tot = run_batches(ctx, descs[:3000], 1000)
             rec = ctx.staged_stats()
@@ -184,7 +184,7 @@ def test_staged_scrambled_wire_mode():
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
     for batch in (n, 64):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_STAGED, opts=X.OPT_ALL) as ctx:
             v, r, tot = run_batches(ctx, descs, batch)
             rec = ctx.staged_stats()
@@ -201,7 +201,7 @@ def test_staged_scrambled_multi_context():
     _dev()
     n = 2 * CHUNK + 999
     umem, descs = scrambled(n, n + 4096, 2048, 256, 0x5EED4D4D, mode=1, lo=20, hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.MultiContext(work, [0, 0], max_batch=n, mode=X.MODE_STAGED) as m:
         v, r, st = m.process(descs)
     check(umem, work, descs, v, r, {k: int(st[k]) for k in COUNTERS})
@@ -213,7 +213,7 @@ def test_staged_scrambled_rx_loop_shape():
     spans only (the old span fallback copied up to the whole 16 MiB per call)."""
     _dev()
     umem, descs = scrambled(4096, 4096, 4096, 256, 0x5EED4E4E, mode=1, lo=20, hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_STAGED) as ctx:
         v, r, tot = run_batches(ctx, descs, 64)
         rec = ctx.staged_stats()
@@ -242,7 +242,7 @@ def test_staged_packed_reordered_aligned_tail():
     plans = SP.call_plans(descs, umem.nbytes)
     assert plans[-1][2] and not any(p[1] for p in plans)
     for rep in range(3):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
             v, r, st = ctx.process(descs)
             rec = ctx.staged_stats()
@@ -278,7 +278,7 @@ def test_staged_2d_rows_past_short_frames():
     plans = SP.call_plans(descs, umem.nbytes)
     assert plans[0][1] and all(p[0] == SP.TWO_D and not p[1] for p in plans[1:]), plans
     for rep in range(3):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
             v, r, st = ctx.process(descs)
             rec = ctx.staged_stats()
@@ -301,7 +301,7 @@ def test_staged_wire_64b_pitch_interleaved():
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
     plans = SP.call_plans(descs, umem.nbytes, wire=True)
     for rep in range(2):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED, opts=X.OPT_ALL) as ctx:
             v, r, st = ctx.process(descs)
             rec = ctx.staged_stats()
@@ -320,7 +320,7 @@ def test_staged_no_alias_rx_loop_shape():
     UMEM per call)."""
     _dev()
     umem, descs = scrambled(4096, 4096, 4096, 256, 0x5EED5D5D, mode=1, lo=20, hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_STAGED) as ctx:
         ctx.drop_alias()
         v, r, tot = run_batches(ctx, descs, 64)
@@ -339,7 +339,7 @@ def test_staged_no_alias_multi_chunk_and_jumbo():
     _dev()
     n = 3 * CHUNK + 777
     umem, descs = scrambled(n, n + n // 4, 2048, 0, 0x5EED5E5E, mode=1, lo=20, hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
         ctx.drop_alias(64 << 10)
         v, r, st = ctx.process(descs)
@@ -357,7 +357,7 @@ def test_staged_no_alias_multi_chunk_and_jumbo():
     big = rng.random(m) < 0.3
     d["len"][big] = 9000
     d = np.ascontiguousarray(d[rng.permutation(m)])
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=m, mode=X.MODE_STAGED) as ctx:
         ctx.drop_alias(8192)
         v, r, st = ctx.process(d)
@@ -377,7 +377,7 @@ def test_staged_no_alias_unaligned_wire_and_umem_end():
     lens = np.random.default_rng(78).integers(1537, 1552, n).astype(np.uint32)
     umem, descs = packed(lens, 0x5EED6363)
     descs = np.ascontiguousarray(descs[np.concatenate([np.arange(c, n, 3) for c in range(3)])])
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
         ctx.drop_alias(1 << 20)
         v, r, st = ctx.process(descs)
@@ -390,7 +390,7 @@ def test_staged_no_alias_unaligned_wire_and_umem_end():
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, X.OPT_ALL)
     for batch in (n, 64):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_STAGED, opts=X.OPT_ALL) as ctx:
             ctx.drop_alias()
             v, r, tot = run_batches(ctx, descs, batch)
@@ -411,7 +411,7 @@ def test_staged_no_alias_unaligned_wire_and_umem_end():
             umem[a:] = tmp[:length]
             descs = np.zeros(1, X.DESC_DTYPE)
             descs[0] = (a, length, 0)
-            work = umem.copy()
+            work = X.umem_copy(umem)
             with X.EchoContext(work, 0, max_batch=4096, mode=X.MODE_STAGED) as ctx:
                 if not alias:
                     ctx.drop_alias()
@@ -426,7 +426,7 @@ def test_staged_no_alias_multi_context():
     _dev()
     n = 2 * CHUNK + 999
     umem, descs = scrambled(n, n + 4096, 2048, 256, 0x5EED6060, mode=1, lo=20, hi=1500)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.MultiContext(work, [0, 0], max_batch=n, mode=X.MODE_STAGED) as m:
         m.drop_alias()
         v, r, st = m.process(descs)
@@ -450,7 +450,7 @@ def test_lowlat_timeout_exactly_once():
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
     outcomes = []
     for rep in range(6):
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.EchoContext(work, 0, max_batch=1024, mode=X.MODE_LOWLAT) as ctx:
             if rep % 2:
                 ctx.process(descs[:1])  # the grid is up and idle (vs. launched by the call itself)
@@ -482,6 +482,47 @@ def test_lowlat_timeout_exactly_once():
     print("timeout outcomes:", outcomes)
 
 
+def test_lowlat_late_completion_deterministic():
+    """the late-completion path, made to happen.  The grid is resident and idle; a 1024 x 1500-B batch
+    over four workgroups takes ~42 us, and the completion timeout is 15 us, so STOP is posted after every workgroup has
+    taken its slice (they poll every ~0.7 us) and before any has finished: all four slices are served, the call returns 0
+    after all (a late completion) with its verdicts and records copied from the channel's buffers after the grid has
+    stopped.  Every rep uses new frames, so a record or verdict left from an earlier batch cannot pass for this one:
+    every verdict, record, byte and counter against the oracle, 20 times."""
+    _dev()
+    n = 1024
+    late = 0
+    umem0 = np.zeros(n * 2048, np.uint8)
+    oracle.synth_batch(umem0, 1, 0, 2048, seed=1, mode=0)
+    work = X.umem_zeros(n * 2048)
+    with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_LOWLAT) as ctx:
+        assert ctx.mode == X.MODE_LOWLAT
+        for rep in range(20):
+            umem = np.zeros(n * 2048, np.uint8)
+            descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED7100 + rep, mode=1, len_lo=1400, len_hi=1500)
+            ref = umem.copy()
+            v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
+            work[:] = umem0
+            ctx.lowlat_tune(timeout_us=0)
+            ctx.process(np.ascontiguousarray(descs[:1]))  # the grid is up and idle
+            work[:] = umem
+            before = ctx.lowlat_outcomes()
+            ctx.lowlat_tune(groups=4, timeout_us=15)
+            v, r, st = ctx.process(descs)
+            out = ctx.lowlat_outcomes()
+            late += out["late"] - before["late"]
+            assert out["partial"] == before["partial"] and out["untouched"] == before["untouched"], (rep, out)
+            bad = np.nonzero(r != r_ref)[0]
+            assert (v == v_ref).all() and len(bad) == 0, (rep, out, f"{len(bad)} records differ", bad[:8].tolist())
+            diff = np.nonzero(work != ref)[0]
+            assert len(diff) == 0, (rep, out, describe_diff(umem, work, ref, descs, v, diff, ctx))
+            for k in COUNTERS:
+                assert int(st[k]) == int(s_ref[k]), k
+        ctx.lowlat_tune(groups=0, timeout_us=0)
+    assert late >= 15, f"only {late} of 20 batches completed late (the path under test)"
+    print(f"late completions: {late} of 20")
+
+
 def test_lowlat_partial_timeout_deterministic():
     """the partly-served timeout path, made to happen.  The resident grid is launched with two workgroups
     (test switch) while a 1024 x 1500-B batch is posted for four: slices 0 and 1 are served, 2 and 3 never are.  At the
@@ -494,14 +535,14 @@ def test_lowlat_partial_timeout_deterministic():
     descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED6161, mode=1, len_lo=20, len_hi=1500)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch(ref, descs)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_LOWLAT) as ctx:
         assert ctx.mode == X.MODE_LOWLAT
         ctx.lowlat_tune(groups=4, timeout_us=20000)
         ctx.lowlat_test_width(2)
         v, r, st = ctx.process(descs)
         out = ctx.lowlat_outcomes()
-        assert out == {"timeouts": 1, "partial": 1, "untouched": 0}, out
+        assert out == {"timeouts": 1, "partial": 1, "untouched": 0, "late": 0}, out
         assert (v == v_ref).all() and (r == r_ref).all() and (work == ref).all()
         for k in COUNTERS:
             assert int(st[k]) == int(s_ref[k]), k
@@ -512,7 +553,7 @@ def test_lowlat_partial_timeout_deterministic():
         ref2 = umem.copy()
         v2_ref, r2_ref, _ = oracle.echo_batch(ref2, mid)
         v, r, _ = ctx.process(mid)
-        assert ctx.lowlat_outcomes() == {"timeouts": 2, "partial": 2, "untouched": 0}
+        assert ctx.lowlat_outcomes() == {"timeouts": 2, "partial": 2, "untouched": 0, "late": 0}
         assert (v == v2_ref).all() and (r == r2_ref).all() and (work == ref2).all()
         ctx.lowlat_test_width(0)
         ctx.lowlat_tune(groups=0, timeout_us=0)
@@ -541,7 +582,7 @@ def test_lowlat_reserved_queue_for_an_application_stream():
             descs = oracle.synth_batch(umem, 512, 256, 4096, 0x5EED5050 + q, mode=1, len_lo=20, len_hi=1500)
             umems.append(umem)
             descss.append(descs)
-            ctxs.append(X.EchoContext(umem.copy(), 0, max_batch=64, mode=X.MODE_LOWLAT))
+            ctxs.append(X.EchoContext(X.umem_copy(umem), 0, max_batch=64, mode=X.MODE_LOWLAT))
         modes = [c.mode for c in ctxs]
         k = modes.count(X.MODE_LOWLAT)
         assert k <= cap and modes == [X.MODE_LOWLAT] * k + [X.MODE_ZEROCOPY] * (4 - k), (cap, modes)
@@ -579,7 +620,7 @@ def test_multi_lowlat_with_downgraded_contexts():
         n = 64 * 40
         umem = np.zeros(n * 2048, np.uint8)
         descs = oracle.synth_batch(umem, n, 0, 2048, seed=0x5EED5151, mode=1, len_lo=20, len_hi=1500)
-        work = umem.copy()
+        work = X.umem_copy(umem)
         with X.MultiContext(work, [0, 0, 0], max_batch=192, mode=X.MODE_LOWLAT) as m:
             v, r, tot = run_batches(m, descs, 192)
         check(umem, work, descs, v, r, tot)

@@ -112,7 +112,7 @@ def test_wire_host_umem_modes(mode):
     umem, descs = mixed_batch(3000, 2048, seed=5, offsets=True)
     ref = umem.copy()
     v_ref, r_ref, s_ref = oracle.echo_batch_opts(ref, descs, 7)
-    work = umem.copy()
+    work = X.umem_copy(umem)
     with X.EchoContext(work, 0, max_batch=1024, mode=mode, opts=7) as ctx:
         vs, rs, tx = [], [], 0
         for i in range(0, len(descs), 1024):

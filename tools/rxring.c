@@ -28,7 +28,16 @@
  * empty=1: the empty-ring latency instead -- the NIC delivers exactly <step> frames, the step serves them, repeat
  * (each call finds exactly its batch: the RX-loop latency of tools/hostlat.py, through the ring loop).
  * Prints one JSON line: Mframes/s per queue and in total (frames / the timed application time), us per step (mean,
- * p50, p99), frames checked, failures.  Tool only: it builds its own frames and links only libxsknet_amd.
+ * p50, p99), frames checked, and the frames not answered by cause:
+ *   tx_full      replies the step produced but dropped because the TX ring was full (xsk_receive.c:178-181's path;
+ *                the NIC thread had not taken the earlier ones yet) -- not a wrong result;
+ *   not_replied  frames handed back with a verdict other than TX_REPLY: every frame is an echo request, so a wrong
+ *                verdict;
+ *   wrong_reply  transmitted replies whose bytes differ from the exact echo reply (or whose length does);
+ *   counters     1 if the step counters disagree with the frames completed (tx_packets must equal the replies sent);
+ * failures = not_replied + wrong_reply + counters (the correctness failures only).  A dropped frame's header, read when
+ * it comes back on the fill ring, is also sorted into request / reply / other (dropped_req_rep_other): a TX-full drop
+ * holds the reply, a wrong verdict the request.  Tool only: it builds its own frames and links only libxsknet_amd.
  */
 #define _GNU_SOURCE
 #include <pthread.h>
@@ -115,7 +124,7 @@ static void ring_init(struct xsk_gpu_ring* r, struct ring_mem* m, uint32_t size,
 }
 
 xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i); /* (library hook: a pipe's context) */
-int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[3]); /* (library hook: LOWLAT call outcomes) */
+int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[4]); /* (library hook: LOWLAT call outcomes) */
 
 struct queue {
     uint32_t q, step, len, ring, frames, empty, pipe, nic_thread, huge;
@@ -123,8 +132,9 @@ struct queue {
     double seconds;
     /* results */
     uint64_t frames_done, steps, checked, fail;
+    uint64_t tx_full, not_replied, wrong_reply, counters; /* the unanswered frames by cause (fail = the last three) */
     uint64_t dropped[3]; /* frames handed back without a reply: header still the request / the reply / other */
-    uint64_t outcomes[3]; /* LOWLAT batches past their timeout: all, completed partly served, failed (xsk_gpu__lowlat_outcomes) */
+    uint64_t outcomes[4]; /* LOWLAT batches past their timeout: all, completed partly served, failed, late (xsk_gpu__lowlat_outcomes) */
     double busy, wall;
     double* lat;
     uint64_t nlat;
@@ -146,7 +156,7 @@ struct nic {
     uint8_t* primed; /* per chunk: the full request was written once (later only its header is restored) */
     uint8_t* out;    /* per chunk: delivered on RX and not yet seen on TX */
     volatile int stop;
-    uint64_t checked, fail;
+    uint64_t checked, fail;  /* fail: transmitted replies of the wrong length or bytes */
 };
 
 /* One pass: every reply on the TX ring completed, its frame checked against the exact echo reply of the request
@@ -307,7 +317,8 @@ static void* run_queue(void* arg) {
                 break;
             }
             if (got == 0) continue;
-            if (res.replied != (uint32_t)got || res.tx_full) Q->fail += (uint64_t)got - res.replied;
+            Q->tx_full += res.tx_full;
+            Q->not_replied += (uint64_t)got - res.replied - res.tx_full;
             done += (uint64_t)got;
             Q->steps++;
             if (Q->nlat < cap) Q->lat[Q->nlat++] = now_s() - s0;
@@ -331,7 +342,8 @@ static void* run_queue(void* arg) {
         }
         Q->busy += dt;
         if (got == 0) continue;
-        if (res.replied != (uint32_t)got || res.tx_full) Q->fail += (uint64_t)got - res.replied;
+        Q->tx_full += res.tx_full;
+        Q->not_replied += (uint64_t)got - res.replied - res.tx_full;
         Q->frames_done += (uint64_t)got;
         Q->steps++;
         Q->lat[Q->nlat++] = dt;
@@ -341,8 +353,13 @@ static void* run_queue(void* arg) {
         struct xsk_gpu_rx_result res;
         const int got = xsk_gpu_rx_pipe_flush(pipe, &tx, &pool, &st, &res);
         Q->busy += now_s() - t0;
-        if (got < 0) Q->rc = got;
-        else Q->frames_done += (uint64_t)got;
+        if (got < 0) {
+            Q->rc = got;
+        } else {
+            Q->tx_full += res.tx_full;
+            Q->not_replied += (uint64_t)got - res.replied - res.tx_full;
+            Q->frames_done += (uint64_t)got;
+        }
     }
     Q->wall = Q->nic_thread == 2 ? Q->busy : now_s() - t_start;
     if (Q->nic_thread == 1) {
@@ -352,15 +369,17 @@ static void* run_queue(void* arg) {
         nic_pass(&N);
     }
     Q->checked = N.checked;
-    Q->fail += N.fail;
+    Q->wrong_reply = N.fail;
     for (uint32_t i = 0; i < (pipe ? Q->pipe : 1u); i++) { /* LOWLAT outcomes, every context of the queue */
-        uint64_t o[3];
+        uint64_t o[4];
         if (xsk_gpu__lowlat_outcomes(pipe ? xsk_gpu__rx_pipe_ctx(pipe, i) : ctx, o) == 0)
-            for (int k = 0; k < 3; k++) Q->outcomes[k] += o[k];
+            for (int k = 0; k < 4; k++) Q->outcomes[k] += o[k];
     }
     if (pipe) xsk_gpu_rx_pipe_fini(pipe);
     xsk_gpu_fini(ctx);
-    if (st.rx_packets != Q->frames_done || st.tx_packets != Q->frames_done) Q->fail++;
+    /* a reply dropped for a full TX ring is not counted as sent (xsk_receive.c:171-172 count successful sends) */
+    if (st.rx_packets != Q->frames_done || st.tx_packets != Q->frames_done - Q->tx_full - Q->not_replied) Q->counters = 1;
+    Q->fail = Q->not_replied + Q->wrong_reply + Q->counters;
     free(N.primed);
     free(N.out);
     if (Q->huge) xsk_gpu_umem_free(umem, (uint64_t)F * CHUNK);
@@ -414,7 +433,7 @@ int main(int argc, char** argv) {
         Q[q].seconds = seconds;
         pthread_create(&th[q], NULL, run_queue, &Q[q]);
     }
-    uint64_t tot = 0, checked = 0, fail = 0;
+    uint64_t tot = 0, checked = 0, fail = 0, tx_full = 0;
     double t_max = 0.0;
     int rc = 0;
     printf("{\"tool\": \"rxring\", \"step\": %u, \"mode\": \"%s\", \"len\": %u, \"queues\": %u, \"ring\": %u, "
@@ -428,22 +447,25 @@ int main(int argc, char** argv) {
         const double p50 = R->nlat ? R->lat[R->nlat / 2] : 0.0, p99 = R->nlat ? R->lat[(R->nlat * 99) / 100] : 0.0;
         const double T = nic ? R->wall : R->busy; /* the NIC in a thread of its own: the loop's wall time */
         printf("%s{\"mode\": %d, \"mframes_s\": %.3f, \"us_per_step\": %.3f, \"p50_us\": %.3f, \"p99_us\": %.3f, "
-               "\"frames_per_step\": %.1f, \"steps\": %llu, \"dropped_req_rep_other\": [%llu, %llu, %llu], "
-               "\"lowlat_timeouts_all_partial_failed\": [%llu, %llu, %llu], \"rc\": %d}", q ? ", " : "", R->real_mode,
+               "\"frames_per_step\": %.1f, \"steps\": %llu, \"tx_full\": %llu, \"not_replied\": %llu, "
+               "\"wrong_reply\": %llu, \"counters\": %llu, \"dropped_req_rep_other\": [%llu, %llu, %llu], "
+               "\"lowlat_timeouts_all_partial_failed_late\": [%llu, %llu, %llu, %llu], \"rc\": %d}", q ? ", " : "", R->real_mode,
                T > 0 ? 1e-6 * (double)R->frames_done / T : 0.0, R->steps ? 1e6 * T / (double)R->steps : 0.0, 1e6 * p50,
                1e6 * p99,
                R->steps ? (double)R->frames_done / (double)R->steps : 0.0, (unsigned long long)R->steps,
-               (unsigned long long)R->dropped[0], (unsigned long long)R->dropped[1], (unsigned long long)R->dropped[2],
+               (unsigned long long)R->tx_full, (unsigned long long)R->not_replied, (unsigned long long)R->wrong_reply,
+               (unsigned long long)R->counters, (unsigned long long)R->dropped[0], (unsigned long long)R->dropped[1], (unsigned long long)R->dropped[2],
                (unsigned long long)R->outcomes[0], (unsigned long long)R->outcomes[1],
-               (unsigned long long)R->outcomes[2], R->rc);
+               (unsigned long long)R->outcomes[2], (unsigned long long)R->outcomes[3], R->rc);
         tot += R->frames_done;
         checked += R->checked;
         fail += R->fail;
+        tx_full += R->tx_full;
         if ((nic ? R->wall : R->busy) > t_max) t_max = nic ? R->wall : R->busy;
         free(R->lat);
     }
-    printf("], \"mframes_s_total\": %.3f, \"frames\": %llu, \"checked\": %llu, \"failures\": %llu, \"rc\": %d}\n",
-           t_max > 0 ? 1e-6 * (double)tot / t_max : 0.0, (unsigned long long)tot, (unsigned long long)checked,
-           (unsigned long long)fail, rc);
+    printf("], \"mframes_s_total\": %.3f, \"frames\": %llu, \"checked\": %llu, \"tx_full\": %llu, \"failures\": %llu, "
+           "\"rc\": %d}\n", t_max > 0 ? 1e-6 * (double)tot / t_max : 0.0, (unsigned long long)tot,
+           (unsigned long long)checked, (unsigned long long)tx_full, (unsigned long long)fail, rc);
     return rc || fail ? 1 : 0;
 }

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 import errno as _errno
+import mmap
 import os
 from typing import Optional
 
@@ -288,6 +289,22 @@ def lowlat_live(device: int = 0) -> int:
     return int(out.value)
 
 
+def umem_zeros(nbytes: int) -> np.ndarray:
+    """A zeroed host UMEM on pages of its own: an anonymous mapping, so its base is page-aligned as xsk_gpu_init /
+    xsk_gpu_multi_init / xsk_gpu_rx_pipe_init require and AF_XDP does -- the counterpart of the reference's
+    posix_memalign(getpagesize(), ...) (src/lib/xsk_utils.c:132-135).  A plain numpy array is not: its data may start
+    inside a page another allocation shares."""
+    nbytes = int(nbytes)
+    return np.frombuffer(mmap.mmap(-1, max(nbytes, 1)), np.uint8, count=nbytes)
+
+
+def umem_copy(a: np.ndarray) -> np.ndarray:
+    """umem_zeros of a's size holding a's bytes."""
+    out = umem_zeros(a.nbytes)
+    out[:] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+    return out
+
+
 class HugeUmem:
     """xsk_gpu_umem_alloc / xsk_gpu_umem_free: a UMEM on transparent huge pages (2 MiB aligned, touched up front);
     `.array` is its numpy uint8 view, `.huge_bytes` how much of it the kernel backed with huge pages."""
@@ -387,10 +404,10 @@ class EchoContext:
 
     def lowlat_outcomes(self):
         """xsk_gpu__lowlat_outcomes: doorbell batches that missed their timeout -- all, completed through the launch
-        path after a partial service, returned -ETIMEDOUT."""
-        out = (C.c_uint64 * 3)()
+        path after a partial service, returned -ETIMEDOUT, completed late (every slice served, found after STOP)."""
+        out = (C.c_uint64 * 4)()
         _check("xsk_gpu__lowlat_outcomes", lib().xsk_gpu__lowlat_outcomes(self._ctx, out))
-        return {"timeouts": int(out[0]), "partial": int(out[1]), "untouched": int(out[2])}
+        return {"timeouts": int(out[0]), "partial": int(out[1]), "untouched": int(out[2]), "late": int(out[3])}
 
     def rx_step(self, rx: Ring, fill: Ring, tx: Ring, pool: FramePool, max_batch: int, stats=None):
         """xsk_gpu_rx_step on this context; returns (received, RxResult)."""

@@ -82,14 +82,18 @@ struct xsk_gpu_ctx {
     int registered;   /* this context registered the UMEM (and unregisters it at fini) */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
-    uint64_t ll_outcome[3]; /* LOWLAT doorbell batches that timed out: all, completed through the launch path after a
-                             * partial service, returned -ETIMEDOUT (xsk_gpu__lowlat_outcomes) */
+    uint64_t ll_outcome[4]; /* LOWLAT doorbell batches that missed their timeout: all, completed through the launch path
+                             * after a partial service, returned -ETIMEDOUT, completed late (every slice served,
+                             * found after STOP) -- xsk_gpu__lowlat_outcomes */
     /* the batch xsk_gpu__submit put in flight and xsk_gpu__complete has not taken back yet */
     uint32_t pend_n;      /* its frames; 0: none */
     int pend_bell;        /* on the doorbell (else launched) */
     uint32_t pend_w;      /* doorbell: its serving workgroups */
     uint32_t pend_chunks; /* launched: its chunks */
     int pend_recs;        /* records asked for */
+    /* the last failed submit / complete: 1 when every frame of its batch is known untouched (it may be submitted
+     * again), 0 when some may have been transformed (xsk_gpu__failed_untouched) */
+    int fail_untouched;
 };
 
 /* LOWLAT contexts per device in this process (include/xsk_gpu.h, XSK_GPU_LOWLAT_PER_DEVICE): a slot is taken at
@@ -235,7 +239,7 @@ static void fini_impl(xsk_gpu_ctx* c) {
 static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode,
                      int prereg) {
     int rc = 0;
-    if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || max_batch == 0 ||
+    if (!out || !umem || umem_size == 0 || !xsk_gpu__umem_aligned(umem) || (umem_size & 15u) || max_batch == 0 ||
         max_batch > XSK_GPU_MAX_BATCH ||
         (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED && mode != XSK_GPU_MODE_LOWLAT))
         return -EINVAL;
@@ -367,9 +371,9 @@ int xsk_gpu__staged_noalias(xsk_gpu_ctx* c, uint32_t half_bytes) {
     return 0;
 }
 int xsk_gpu_ctx_mode(const xsk_gpu_ctx* c) { return c ? c->mode : -EINVAL; }
-int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[3]) {
+int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[4]) {
     if (!c || !out || !c->ll) return -EINVAL;
-    for (int i = 0; i < 3; i++) out[i] = c->ll_outcome[i];
+    for (int i = 0; i < 4; i++) out[i] = c->ll_outcome[i];
     return 0;
 }
 xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* c) { return c ? c->ll : NULL; }
@@ -572,6 +576,7 @@ int xsk_gpu__process_ex(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32
 int xsk_gpu__submit(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n, int want_recs, int no_doorbell) {
     int rc = 0;
     if (!c || (!descs && n)) return -EINVAL;
+    c->fail_untouched = 1; /* every failure below before a batch is posted or a chunk enqueued */
     if (c->pend_n) return -EBUSY; /* one batch in flight per context */
     if (n == 0) return 0;
     if (n > c->max_batch) return -EINVAL;
@@ -584,7 +589,11 @@ int xsk_gpu__submit(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
         memcpy(xsk_gpu__lowlat_descs(c->ll), descs, (size_t)n * sizeof *descs);
         uint32_t w = 0;
         rc = xsk_gpu__lowlat_post(c->ll, n, want_recs, &w);
-        if (rc) return rc;
+        if (rc) {
+            /* posted, then the relaunch failed: a later instance could still serve it (the channel is broken) */
+            c->fail_untouched = !xsk_gpu__lowlat_broken(c->ll);
+            return rc;
+        }
         c->pend_n = n;
         c->pend_bell = 1;
         c->pend_w = w;
@@ -603,6 +612,7 @@ int xsk_gpu__submit(xsk_gpu_ctx* c, const struct xsk_gpu_desc* descs, uint32_t n
         rc = enqueue_chunk(c, descs, i0, m, nchunks, want_recs, (int)(nchunks % NSTREAMS), &prefix_aligned);
         if (rc) {
             for (int s = 0; s < NSTREAMS; s++) (void)hipStreamSynchronize(c->stream[s]);
+            c->fail_untouched = 0; /* chunks before this one, or this one's kernel, may have run */
             goto out;
         }
         i0 += m;
@@ -615,6 +625,8 @@ out:
     if (caller_dev >= 0 && caller_dev != c->device) (void)hipSetDevice(caller_dev);
     return rc;
 }
+
+int xsk_gpu__failed_untouched(const xsk_gpu_ctx* c) { return c && c->fail_untouched; }
 
 int xsk_gpu__ready(const xsk_gpu_ctx* c) {
     if (!c || !c->pend_n) return 1;
@@ -635,7 +647,12 @@ static int complete_doorbell(xsk_gpu_ctx* c, uint32_t n, uint8_t* verdicts, stru
      * completes, every frame transformed exactly once */
     const int partial = rc == -ETIMEDOUT && !xsk_gpu__lowlat_broken(c->ll) && unserved && unserved != (1u << w) - 1u;
     if (rc == -ETIMEDOUT) c->ll_outcome[partial ? 1 : 2]++, c->ll_outcome[0]++;
-    if (rc && !partial) return rc;
+    if (!rc && xsk_gpu__lowlat_last_late(c->ll)) c->ll_outcome[3]++, c->ll_outcome[0]++;
+    if (rc && !partial) {
+        /* every slice untouched (the channel stopped without serving any) or the outcome unknown (broken) */
+        c->fail_untouched = rc == -ETIMEDOUT && !xsk_gpu__lowlat_broken(c->ll) && unserved == (1u << w) - 1u;
+        return rc;
+    }
     uint8_t hv[XSK_GPU_LOWLAT_MAX];
     memcpy(hv, xsk_gpu__lowlat_verdicts(c->ll), n);
     if (recs) memcpy(recs, xsk_gpu__lowlat_recs(c->ll), (size_t)n * sizeof *recs);
@@ -645,7 +662,10 @@ static int complete_doorbell(xsk_gpu_ctx* c, uint32_t n, uint8_t* verdicts, stru
         xsk_gpu__ll_slice(n, w, g, &f0, &f1);
         if (f1 <= f0) continue;
         rc = xsk_gpu__process_ex(c, descs + f0, f1 - f0, hv + f0, recs ? recs + f0 : NULL, NULL, 1);
-        if (rc) return rc;
+        if (rc) {
+            c->fail_untouched = 0; /* the grid served the other slices */
+            return rc;
+        }
     }
     if (verdicts) memcpy(verdicts, hv, n);
     if (stats) { /* xsk_receive.c:171-172, 229, 233 -- what the kernel's counter phase would add */
@@ -671,6 +691,7 @@ int xsk_gpu__complete(xsk_gpu_ctx* c, uint8_t* verdicts, struct xsk_gpu_rec* rec
     const uint32_t n = c->pend_n;
     if (!n) return 0;
     c->pend_n = 0;
+    c->fail_untouched = 0; /* a failure below: part of the batch may have been transformed */
     if (c->pend_bell) return complete_doorbell(c, n, verdicts, recs, stats);
     if (!c->pend_recs) recs = NULL;
     const struct xsk_gpu_desc* descs = c->h_descs; /* the batch as submitted: every chunk copied it there */

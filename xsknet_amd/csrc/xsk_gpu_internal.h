@@ -5,8 +5,20 @@
 #ifndef XSK_GPU_INTERNAL_H
 #define XSK_GPU_INTERNAL_H
 
+#include <unistd.h>
+
 #include "../../include/xsk_gpu.h"
 #include "xsk_lowlat_proto.h"
+
+/* A host UMEM starts on a page of its own (include/xsk_gpu.h): AF_XDP rejects an area that is not page-aligned and the
+ * reference allocates one with posix_memalign(getpagesize(), ...) (src/lib/xsk_utils.c:132-135).  The runtime registers
+ * whole pages, so a UMEM that began inside a page would share that page's registration -- and its GPU translation --
+ * with whatever else lives there. */
+static inline int xsk_gpu__umem_aligned(const void* umem) {
+    long pg = sysconf(_SC_PAGESIZE);
+    if (pg <= 0) pg = 4096;
+    return ((uintptr_t)umem % (uintptr_t)pg) == 0;
+}
 
 #ifdef __cplusplus
 extern "C" {
@@ -123,12 +135,19 @@ XSK_GPU__HIDDEN int xsk_gpu__submit(xsk_gpu_ctx* ctx, const struct xsk_gpu_desc*
 XSK_GPU__HIDDEN int xsk_gpu__complete(xsk_gpu_ctx* ctx, uint8_t* verdicts, struct xsk_gpu_rec* recs,
                                       struct xsk_gpu_stats* stats);
 XSK_GPU__HIDDEN int xsk_gpu__ready(const xsk_gpu_ctx* ctx);
+/* After a failed xsk_gpu__submit / xsk_gpu__complete / xsk_gpu_process: 1 when every frame of that batch is known to be
+ * untouched -- nothing was posted or launched, or a doorbell batch timed out and the stopped grid had served none of it
+ * -- so the batch may be run again; 0 when some frames may have been transformed (a partly served batch whose launch
+ * path failed, a launch error, a channel still running after its timeout): running it again could transform a frame
+ * twice (a request already turned into a reply reads as DROP_NOT_ECHO), so the RX loops drop such a batch instead. */
+XSK_GPU__HIDDEN int xsk_gpu__failed_untouched(const xsk_gpu_ctx* ctx);
 
 /* xsk_gpu_rx.c, shared by xsk_gpu_rx_step and the pipelined loop (xsk_gpu_pipe.c): stock the fill ring from the
  * free-frame stack (src/lib/xsk_receive.c:201-217; returns the frames handed over), and hand a transformed batch on --
  * replies onto the TX ring while it has room, every other frame back to the pool, the counters (:171-186, :226-233);
  * r->replied and r->tx_full accumulate. */
 XSK_GPU__HIDDEN uint32_t xsk_gpu__rx_refill(struct xsk_gpu_ring* fill, struct xsk_gpu_frame_pool* pool);
+XSK_GPU__HIDDEN void xsk_gpu__rx_drop(const struct xsk_gpu_desc* descs, uint32_t n, struct xsk_gpu_frame_pool* pool);
 XSK_GPU__HIDDEN void xsk_gpu__rx_emit(const struct xsk_gpu_desc* descs, const uint8_t* verdict, uint32_t n,
                                       struct xsk_gpu_ring* tx, struct xsk_gpu_frame_pool* pool,
                                       struct xsk_gpu_stats* stats, struct xsk_gpu_rx_result* r);
@@ -200,6 +219,8 @@ XSK_GPU__HIDDEN int xsk_gpu__lowlat_set_opts(xsk_gpu__lowlat* ll, uint32_t opts)
 XSK_GPU__HIDDEN void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll);
 /* 1 while a timed-out batch's instance has not stopped (later calls return -EBUSY). */
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_broken(xsk_gpu__lowlat* ll);
+/* The last wait returned 0 for a batch past its timeout (a late completion: every slice served, found after STOP). */
+XSK_GPU__HIDDEN int xsk_gpu__lowlat_last_late(const xsk_gpu__lowlat* ll);
 /* A broken channel whose instance has stopped by now becomes usable again: returns 1 if the channel is usable
  * (never broken, or recovered), 0 while the instance still runs.  Never blocks. */
 XSK_GPU__HIDDEN int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll);
@@ -221,7 +242,7 @@ XSK_GPU__HIDDEN xsk_gpu__lowlat* xsk_gpu__ctx_lowlat(xsk_gpu_ctx* ctx);
 /* xsk_gpu_host.c (exported for the GPU tests, not part of the ABI): a LOWLAT context's doorbell batches that missed their
  * completion timeout since init -- out[0] all of them, out[1] those completed through the launch path after the
  * resident grid had served part of them, out[2] those returned as -ETIMEDOUT.  -EINVAL for other modes. */
-int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* ctx, uint64_t out[3]);
+int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* ctx, uint64_t out[4]);
 /* xsk_lowlat.hip (test switch, not part of the ABI): the resident grid is launched with `wgs` workgroups (1 ..
  * XSK_GPU__LL_WG; 0 = all) from the next batch on, while batches are still posted for as many workgroups as their size
  * asks (xsk_gpu__lowlat_tune's `groups`): slices of workgroups that do not exist are never served, which makes a batch

@@ -127,7 +127,7 @@ void xsk_gpu_multi_fini(xsk_gpu_multi* m) {
 
 int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, void* umem, uint64_t umem_size,
                        uint32_t max_batch, int mode) {
-    if (!out || !devices || ndev == 0 || ndev > XSK_GPU_MULTI_MAX || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) ||
+    if (!out || !devices || ndev == 0 || ndev > XSK_GPU_MULTI_MAX || !umem || umem_size == 0 || !xsk_gpu__umem_aligned(umem) ||
         (umem_size & 15u) || max_batch == 0 || max_batch > XSK_GPU_MAX_BATCH ||
         (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED && mode != XSK_GPU_MODE_LOWLAT))
         return -EINVAL;

@@ -19,7 +19,8 @@
 struct pipe_slot {
     xsk_gpu_ctx* ctx;
     uint32_t n;  /* frames of the batch this context holds (0: free) */
-    int failed;  /* its completion failed: the next step or flush runs it again through xsk_gpu_process */
+    int failed;  /* its completion failed with every frame untouched: the next step or flush runs it again through
+                  * xsk_gpu_process */
     struct xsk_gpu_desc descs[XSK_GPU_RX_MAX_STEP]; /* the batch as received (the TX / free path needs them) */
     uint8_t verdict[XSK_GPU_RX_MAX_STEP];
 };
@@ -47,7 +48,7 @@ void xsk_gpu_rx_pipe_fini(xsk_gpu_rx_pipe* p) {
 }
 
 int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t umem_size, uint32_t depth, int mode) {
-    if (!out || !umem || umem_size == 0 || ((uintptr_t)umem & 15u) || (umem_size & 15u) || depth == 0 ||
+    if (!out || !umem || umem_size == 0 || !xsk_gpu__umem_aligned(umem) || (umem_size & 15u) || depth == 0 ||
         depth > XSK_GPU_RX_PIPE_MAX ||
         (mode != XSK_GPU_MODE_ZEROCOPY && mode != XSK_GPU_MODE_STAGED && mode != XSK_GPU_MODE_LOWLAT))
         return -EINVAL;
@@ -92,23 +93,35 @@ int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t
     return 0;
 }
 
+static void retire_oldest(xsk_gpu_rx_pipe* p) {
+    struct pipe_slot* s = &p->s[p->head];
+    s->n = 0;
+    s->failed = 0;
+    p->head = (p->head + 1u) % p->depth;
+    p->count--;
+}
+
 /* Complete the oldest batch in flight and hand it on (xsk_gpu_rx_step's steps 4-5): the frames completed, or the
- * error (the batch then stays the oldest, marked to run again). */
+ * error.  A batch that failed with every frame untouched stays the oldest, marked to run again; one whose frames may
+ * partly have been transformed (xsk_gpu__failed_untouched) is dropped -- its frames back to the pool, none transmitted
+ * -- since running it again could transform a frame twice. */
 static int complete_oldest(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* tx, struct xsk_gpu_frame_pool* pool,
                            struct xsk_gpu_stats* stats, struct xsk_gpu_rx_result* r) {
     struct pipe_slot* s = &p->s[p->head];
     const int rc = s->failed ? xsk_gpu_process(s->ctx, s->descs, s->n, s->verdict, NULL, NULL)
                              : xsk_gpu__complete(s->ctx, s->verdict, NULL, NULL);
     if (rc) {
-        s->failed = 1;
+        if (xsk_gpu__failed_untouched(s->ctx)) {
+            s->failed = 1;
+        } else {
+            xsk_gpu__rx_drop(s->descs, s->n, pool);
+            retire_oldest(p);
+        }
         return rc;
     }
     xsk_gpu__rx_emit(s->descs, s->verdict, s->n, tx, pool, stats, r);
     const int n = (int)s->n;
-    s->n = 0;
-    s->failed = 0;
-    p->head = (p->head + 1u) % p->depth;
-    p->count--;
+    retire_oldest(p);
     return n;
 }
 
@@ -125,8 +138,14 @@ int xsk_gpu_rx_pipe_step(xsk_gpu_rx_pipe* p, struct xsk_gpu_ring* rx, struct xsk
         const uint32_t rcvd = xr_cons_peek(rx, max_batch, &idx_rx); /* :196 */
         for (uint32_t i = 0; i < rcvd; i++) s->descs[i] = *xr_desc(rx, idx_rx + i);
         rc = xsk_gpu__submit(s->ctx, s->descs, rcvd, 0, 0);
-        if (rc) { /* frames stay on the RX ring, as after a failed xsk_gpu_rx_step */
-            rx->cached_cons -= rcvd;
+        if (rc) {
+            if (xsk_gpu__failed_untouched(s->ctx)) { /* frames stay on the RX ring, as after a failed xsk_gpu_rx_step */
+                rx->cached_cons -= rcvd;
+            } else { /* possibly partly transformed: dropped, as xsk_gpu_rx_step does */
+                xsk_gpu__rx_drop(s->descs, rcvd, pool);
+                xr_cons_release(rx, rcvd);
+                r.received = rcvd;
+            }
             goto out;
         }
         xr_cons_release(rx, rcvd); /* :232 -- the descriptors are ours now (s->descs) */

@@ -25,6 +25,10 @@ uint32_t xsk_gpu__rx_refill(struct xsk_gpu_ring* fill, struct xsk_gpu_frame_pool
     return stock;
 }
 
+void xsk_gpu__rx_drop(const struct xsk_gpu_desc* descs, uint32_t n, struct xsk_gpu_frame_pool* pool) {
+    for (uint32_t i = 0; i < n; i++) pool_push(pool, descs[i].addr);
+}
+
 void xsk_gpu__rx_emit(const struct xsk_gpu_desc* descs, const uint8_t* verdict, uint32_t n, struct xsk_gpu_ring* tx,
                       struct xsk_gpu_frame_pool* pool, struct xsk_gpu_stats* stats, struct xsk_gpu_rx_result* r) {
     uint32_t nrep = 0;
@@ -84,8 +88,17 @@ int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ri
     for (uint32_t i = 0; i < rcvd; i++) descs[i] = *xr_desc(rx, idx_rx + i);
 
     const int rc = xsk_gpu_process(ctx, descs, rcvd, verdict, NULL, NULL);
-    if (rc) { /* frames stay on the RX ring (not released); the caller may retry or tear down */
-        rx->cached_cons -= rcvd;
+    if (rc) {
+        if (xsk_gpu__failed_untouched(ctx)) { /* frames stay on the RX ring (not released): the caller may retry */
+            rx->cached_cons -= rcvd;
+            return rc;
+        }
+        /* some frames may have been transformed: a retry would transform them twice (a reply reads as
+         * DROP_NOT_ECHO), so the batch is dropped -- its frames go back to the pool, none is transmitted */
+        xsk_gpu__rx_drop(descs, rcvd, pool);
+        xr_cons_release(rx, rcvd);
+        r.received = rcvd;
+        if (res) *res = r;
         return rc;
     }
     xsk_gpu__rx_emit(descs, verdict, rcvd, tx, pool, stats, &r);

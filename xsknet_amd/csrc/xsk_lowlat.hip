@@ -364,6 +364,8 @@ void xsk_gpu__lowlat_stop(xsk_gpu__lowlat* ll) {
 
 int xsk_gpu__lowlat_broken(xsk_gpu__lowlat* ll) { return ll && ll->st.broken; }
 
+int xsk_gpu__lowlat_last_late(const xsk_gpu__lowlat* ll) { return ll && ll->st.last_late; }
+
 int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll) {
     if (!ll || !ll->st.broken) return 1;
     (void)hipSetDevice(ll->device);
@@ -392,10 +394,12 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     xsk_gpu__lowlat* ll = (xsk_gpu__lowlat*)calloc(1, sizeof *ll);
     if (!ll) return -ENOMEM;
     int rc = 0;
-    // the doorbell is fine-grained (polled across PCIe); the data buffers are mapped like the UMEM itself:
-    // the kernel's system-scope acquire / release fences order them
+    // every buffer of the channel is fine-grained: the doorbell and the descriptor slots are polled across PCIe, and the
+    // verdicts and records the host copies out once `done` is seen are stored past the GPU's L2, so their visibility
+    // rests on the stores' own acknowledgements (the wave waits for them before `done`) and not on the L2 write-back
+    // of the release (a late completion once returned exact verdicts with wrong records while these two
+    // were coarse-grained; tests/test_gpu_staged.py::test_lowlat_late_completion_deterministic)
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    const unsigned dfl = hipHostMallocMapped;
 #define LL_TRY(expr)                         \
     do {                                     \
         const hipError_t e_ = (expr);        \
@@ -417,8 +421,8 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     // came back DROP -- profiles/r05/rxpipe_pages.jsonl -- and a slice served from stale descriptors would do exactly
     // that; not seen again in 0.9 G frames either way, profiles/r05/lowlat_slice_recheck.jsonl)
     LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc), fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, dfl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), dfl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, fl));
+    LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), fl));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
     // the descriptor slots too: the leader takes a polled slot as this batch's when its `options` tag equals the
     // batch's seq, and a recycled allocation may still hold an earlier channel's slots tagged 1, 2, 3, ... -- the seqs

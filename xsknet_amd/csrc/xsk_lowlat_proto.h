@@ -119,6 +119,8 @@ struct xsk_gpu__ll_state {
     double quiesce_s;     /* after a timeout, how long to wait for the instance to stop */
     double recheck_s;     /* while waiting, how often to check that an instance is still there */
     int inflight;         /* xsk_gpu__ll_begin posted seq and xsk_gpu__ll_wait has not returned for it yet */
+    int last_late;        /* the last xsk_gpu__ll_wait returned 0 for a batch that had missed its timeout (STOP posted,
+                           * every slice found served once the grid stopped): a late completion */
     uint32_t w_post;      /* its serving workgroups */
     double t_post;        /* when it was posted */
 };
@@ -224,7 +226,13 @@ static inline int xsk_gpu__ll_begin(struct xsk_gpu__ll_state* st, const struct x
         /* the leader was leaving (Dekker: it re-reads the doorbell after clearing alive, or this launch serves
          * the batch) */
         const int rc = ops->launch(ops->u);
-        if (rc) return rc; /* (posted, maybe never served: the next stop / relaunch retires or serves it) */
+        if (rc) {
+            /* posted, and the leader may still have seen it before leaving: the outcome is unknown, so the channel is
+             * broken -- nothing is posted until no instance runs, and then the batch is retired, never served by a
+             * later relaunch behind the caller's back */
+            st->broken = 1;
+            return rc;
+        }
     }
     st->inflight = 1;
     st->w_post = w;
@@ -244,6 +252,7 @@ static inline int xsk_gpu__ll_wait(struct xsk_gpu__ll_state* st, const struct xs
                                    uint32_t* unserved) {
     struct xsk_gpu__bell* b = st->bell;
     if (unserved) *unserved = 0;
+    st->last_late = 0;
     if (!st->inflight) return -EINVAL;
     st->inflight = 0; /* whatever happens below, the batch leaves the channel's hands */
     const uint32_t seq = st->seq, w = st->w_post;
@@ -276,6 +285,7 @@ static inline int xsk_gpu__ll_wait(struct xsk_gpu__ll_state* st, const struct xs
                 /* (ll_stop recorded what the workgroups did with the batch before it retired it) */
                 if (unserved) *unserved = st->stop_unserved;
                 if (st->stop_unserved) return -ETIMEDOUT;
+                st->last_late = 1;
                 break; /* every slice was served, late: a normal completion */
             }
         }
