@@ -21,7 +21,11 @@
  * A step takes min(ring occupancy, step, XSK_GPU_RX_MAX_STEP) frames; the reference's RX_BATCH_SIZE (64,
  * src/lib/xsk_utils.h:8) is a constant of its CPU loop and changes no frame's result.
  *
- *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0] [pipe=0] [nic=thread|inline|burst] [huge=0]
+ *   rxring <step> <lowlat|zerocopy|staged> <seconds> [len=64] [queues=1] [ring=4096] [frames=4096] [empty=0] [pipe=0] [nic=thread|inline|burst] [huge=0] [groups=0]
+ *
+ * groups=G: LOWLAT batches served by G workgroups (xsk_gpu__lowlat_tune; 0 = by size).  The line's `where` lists the
+ * first failures of queue 0 as runs of consecutive slots of one step (step index, slot range, kind: 0 handed back
+ * holding the request, 2 other bytes, 3 a transmitted reply that differs).
  *
  * pipe=D (1..XSK_GPU_RX_PIPE_MAX): the pipelined loop instead -- xsk_gpu_rx_pipe_step() with up to D batches in flight
  * (one context each), a flush at the end; frames count when their batch completes.
@@ -124,10 +128,11 @@ static void ring_init(struct xsk_gpu_ring* r, struct ring_mem* m, uint32_t size,
 }
 
 xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i); /* (library hook: a pipe's context) */
+int xsk_gpu__lowlat_tune(xsk_gpu_ctx* c, uint32_t tile_frames, uint32_t groups, uint32_t timeout_us); /* (hook) */
 int xsk_gpu__lowlat_outcomes(const xsk_gpu_ctx* c, uint64_t out[4]); /* (library hook: LOWLAT call outcomes) */
 
 struct queue {
-    uint32_t q, step, len, ring, frames, empty, pipe, nic_thread, huge;
+    uint32_t q, step, len, ring, frames, empty, pipe, nic_thread, huge, groups;
     int mode, real_mode;
     double seconds;
     /* results */
@@ -139,6 +144,13 @@ struct queue {
     double* lat;
     uint64_t nlat;
     int rc;
+    /* failure locations: each step's first RX sequence number and size, and the first failures' sequence numbers */
+    uint64_t* step_seq;
+    uint32_t* step_n;
+    uint64_t nsteps_logged;
+    uint64_t fail_seq[4096];
+    uint8_t fail_kind[4096]; /* 0 handed back holding the request, 1 holding the reply, 2 other, 3 wrong reply on TX */
+    uint32_t nfail_logged;
 };
 
 static int cmpd(const void* a, const void* b) {
@@ -155,6 +167,7 @@ struct nic {
     uint32_t R, len, k_rx_prod, k_fill_cons, k_tx_cons, k_comp_prod;
     uint8_t* primed; /* per chunk: the full request was written once (later only its header is restored) */
     uint8_t* out;    /* per chunk: delivered on RX and not yet seen on TX */
+    uint64_t* dseq;  /* per chunk: the RX sequence number of its last delivery */
     volatile int stop;
     uint64_t checked, fail;  /* fail: transmitted replies of the wrong length or bytes */
 };
@@ -169,13 +182,26 @@ static void nic_pass(struct nic* N) {
     const uint32_t R = N->R, len = N->len, hdr = len < 64u ? len : 64u;
     const struct xsk_gpu_desc* txe = (const struct xsk_gpu_desc*)N->mtx->ents;
     const uint32_t tx_prod = __atomic_load_n(&N->mtx->prod, __ATOMIC_ACQUIRE);
-    for (; N->k_tx_cons != tx_prod; N->k_tx_cons++) {
+    /* a TX descriptor is taken only while the completion ring has room for it, as the kernel does (round 5's tool
+     * posted completions without looking: with thousands of replies per step it overwrote completions the application
+     * had not read yet, handing the same frames back twice -- every "failure" of its pipelined 1024-frame runs) */
+    const uint32_t comp_cons = __atomic_load_n(&N->mcomp->cons, __ATOMIC_ACQUIRE);
+    uint32_t comp_room = R - (N->k_comp_prod - comp_cons);
+    for (; N->k_tx_cons != tx_prod && comp_room; N->k_tx_cons++, comp_room--) {
         const struct xsk_gpu_desc* d = &txe[N->k_tx_cons & (R - 1)];
         if (tx_prod - N->k_tx_cons > 16u) __builtin_prefetch(N->umem + txe[(N->k_tx_cons + 16u) & (R - 1)].addr);
         N->out[d->addr / CHUNK] = 0;
         const uint64_t k = N->checked++;
-        if (d->len != len) N->fail++;
-        else if ((k & 3u) == 0 && memcmp(N->umem + d->addr, N->rep, (k & 63u) ? hdr : len) != 0) N->fail++;
+        int bad = 0;
+        if (d->len != len) bad = 1;
+        else if ((k & 3u) == 0 && memcmp(N->umem + d->addr, N->rep, (k & 63u) ? hdr : len) != 0) bad = 1;
+        if (bad) {
+            N->fail++;
+            if (N->Q->nfail_logged < 4096) {
+                N->Q->fail_seq[N->Q->nfail_logged] = N->dseq[d->addr / CHUNK];
+                N->Q->fail_kind[N->Q->nfail_logged++] = 3;
+            }
+        }
         ((uint64_t*)N->mcomp->ents)[N->k_comp_prod & (R - 1)] = d->addr;
         N->k_comp_prod++;
     }
@@ -197,9 +223,15 @@ static void nic_pass(struct nic* N) {
         uint8_t* f = N->umem + base + HEADROOM;
         if (N->out[c]) { /* delivered, never transmitted, back on the fill ring: a frame the step did not answer */
             const int is_req = !memcmp(f, N->req, hdr), is_rep = !memcmp(f, N->rep, hdr);
-            N->Q->dropped[is_req ? 0 : is_rep ? 1 : 2]++;
+            const int kind = is_req ? 0 : is_rep ? 1 : 2;
+            N->Q->dropped[kind]++;
+            if (kind != 1 && N->Q->nfail_logged < 4096) { /* (a reply handed back: the TX ring was full) */
+                N->Q->fail_seq[N->Q->nfail_logged] = N->dseq[c];
+                N->Q->fail_kind[N->Q->nfail_logged++] = (uint8_t)kind;
+            }
         }
         N->out[c] = 1;
+        N->dseq[c] = N->k_rx_prod;
         if (N->primed[c] && hdr == 64u) { /* 64-B aligned header, streamed */
             _mm_stream_si128((__m128i*)f, r0);
             _mm_stream_si128((__m128i*)f + 1, r1);
@@ -273,10 +305,16 @@ static void* run_queue(void* arg) {
     N.len = len;
     N.primed = (uint8_t*)calloc(F, 1);
     N.out = (uint8_t*)calloc(F, 1);
+    N.dseq = (uint64_t*)calloc(F, sizeof(uint64_t));
     struct xsk_gpu_stats st;
     memset(&st, 0, sizeof st);
     const size_t cap = 1u << 22;
     Q->lat = (double*)malloc(sizeof(double) * cap);
+    Q->step_seq = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+    Q->step_n = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    if (Q->groups) /* LOWLAT serving workgroups forced (diagnosis: slices vs whole batches) */
+        for (uint32_t i = 0; i < (pipe ? Q->pipe : 1u); i++)
+            (void)xsk_gpu__lowlat_tune(pipe ? xsk_gpu__rx_pipe_ctx(pipe, i) : ctx, 0, Q->groups, 0);
     /* prime the fill ring (the reference's init, xsk_utils.c:163-177) */
     {
         uint32_t idx = 0;
@@ -310,8 +348,13 @@ static void* run_queue(void* arg) {
         while (done < burst) {
             const double s0 = now_s();
             struct xsk_gpu_rx_result res;
+            const uint32_t cons0 = mrx.cons;
             const int got = pipe ? xsk_gpu_rx_pipe_step(pipe, &rx, &fill, &tx, &pool, Q->step, &st, &res)
                                  : xsk_gpu_rx_step(ctx, &rx, &fill, &tx, &pool, Q->step, &st, &res);
+            if (got >= 0 && res.received && Q->nsteps_logged < cap) {
+                Q->step_seq[Q->nsteps_logged] = cons0;
+                Q->step_n[Q->nsteps_logged++] = res.received;
+            }
             if (got < 0) {
                 Q->rc = got;
                 break;
@@ -333,8 +376,13 @@ static void* run_queue(void* arg) {
         const double t0 = now_s();
         xsk_gpu_tx_complete(&comp, &pool, R);
         struct xsk_gpu_rx_result res;
+        const uint32_t cons0 = mrx.cons;
         const int got = pipe ? xsk_gpu_rx_pipe_step(pipe, &rx, &fill, &tx, &pool, Q->step, &st, &res)
                              : xsk_gpu_rx_step(ctx, &rx, &fill, &tx, &pool, Q->step, &st, &res);
+        if (got >= 0 && res.received && Q->nsteps_logged < cap) {
+            Q->step_seq[Q->nsteps_logged] = cons0;
+            Q->step_n[Q->nsteps_logged++] = res.received;
+        }
         const double dt = now_s() - t0;
         if (got < 0) {
             Q->rc = got;
@@ -382,6 +430,7 @@ static void* run_queue(void* arg) {
     Q->fail = Q->not_replied + Q->wrong_reply + Q->counters;
     free(N.primed);
     free(N.out);
+    free(N.dseq);
     if (Q->huge) xsk_gpu_umem_free(umem, (uint64_t)F * CHUNK);
     else free(umem);
     free(pool.addr);
@@ -399,7 +448,7 @@ int main(int argc, char** argv) {
     const int mode = !strcmp(argv[2], "lowlat") ? XSK_GPU_MODE_LOWLAT
                      : !strcmp(argv[2], "staged") ? XSK_GPU_MODE_STAGED : XSK_GPU_MODE_ZEROCOPY;
     const double seconds = atof(argv[3]);
-    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0, pipe = 0, nic = 1, huge = 0;
+    uint32_t len = 64, nq = 1, ring = 4096, frames = 4096, empty = 0, pipe = 0, nic = 1, huge = 0, groups = 0;
     for (int a = 4; a < argc; a++) {
         if (!strncmp(argv[a], "len=", 4)) len = (uint32_t)atoi(argv[a] + 4);
         else if (!strncmp(argv[a], "queues=", 7)) nq = (uint32_t)atoi(argv[a] + 7);
@@ -408,6 +457,7 @@ int main(int argc, char** argv) {
         else if (!strncmp(argv[a], "empty=", 6)) empty = (uint32_t)atoi(argv[a] + 6);
         else if (!strncmp(argv[a], "pipe=", 5)) pipe = (uint32_t)atoi(argv[a] + 5);
         else if (!strncmp(argv[a], "huge=", 5)) huge = (uint32_t)atoi(argv[a] + 5);
+        else if (!strncmp(argv[a], "groups=", 7)) groups = (uint32_t)atoi(argv[a] + 7);
         else if (!strncmp(argv[a], "nic=", 4))
             nic = !strcmp(argv[a] + 4, "thread") ? 1u : !strcmp(argv[a] + 4, "burst") ? 2u : 0u;
     }
@@ -429,11 +479,15 @@ int main(int argc, char** argv) {
         Q[q].pipe = pipe;
         Q[q].nic_thread = nic;
         Q[q].huge = huge;
+        Q[q].groups = groups;
         Q[q].mode = mode;
         Q[q].seconds = seconds;
         pthread_create(&th[q], NULL, run_queue, &Q[q]);
     }
     uint64_t tot = 0, checked = 0, fail = 0, tx_full = 0;
+    /* where the first failures of queue 0 sit: per failing step (by RX sequence), the slot ranges that failed */
+    char where[8192];
+    where[0] = 0;
     double t_max = 0.0;
     int rc = 0;
     printf("{\"tool\": \"rxring\", \"step\": %u, \"mode\": \"%s\", \"len\": %u, \"queues\": %u, \"ring\": %u, "
@@ -442,6 +496,56 @@ int main(int argc, char** argv) {
     for (uint32_t q = 0; q < nq; q++) {
         pthread_join(th[q], NULL);
         struct queue* R = &Q[q];
+        if (q == 0 && R->nfail_logged) {
+            size_t w = 0;
+            uint64_t prev_step = ~0ull;
+            uint32_t run0 = 0, runlen = 0, kind0 = 0;
+            int printed = 0;
+            /* sort the logged failures by sequence number (insertion sort: at most 4096) */
+            for (uint32_t i = 1; i < R->nfail_logged; i++)
+                for (uint32_t j = i; j > 0 && R->fail_seq[j - 1] > R->fail_seq[j]; j--) {
+                    uint64_t t = R->fail_seq[j];
+                    R->fail_seq[j] = R->fail_seq[j - 1];
+                    R->fail_seq[j - 1] = t;
+                    uint8_t k = R->fail_kind[j];
+                    R->fail_kind[j] = R->fail_kind[j - 1];
+                    R->fail_kind[j - 1] = k;
+                }
+            for (uint32_t i = 0; i <= R->nfail_logged && printed < 40 && w < sizeof where - 200; i++) {
+                uint64_t st_i = ~0ull;
+                uint32_t slot = 0, sn = 0;
+                if (i < R->nfail_logged) {
+                    const uint64_t s32 = R->fail_seq[i] & 0xFFFFFFFFull; /* ring indices are u32 */
+                    uint64_t lo = 0, hi = R->nsteps_logged;
+                    while (lo < hi) { /* last step whose start <= seq (steps in RX order; u32 wrap ignored) */
+                        const uint64_t mid = (lo + hi) / 2;
+                        if (R->step_seq[mid] <= s32) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    if (lo) {
+                        st_i = lo - 1;
+                        slot = (uint32_t)(s32 - R->step_seq[st_i]);
+                        sn = R->step_n[st_i];
+                    }
+                }
+                const int cont = i < R->nfail_logged && st_i == prev_step && slot == run0 + runlen &&
+                                 R->fail_kind[i] == kind0;
+                if (cont) {
+                    runlen++;
+                    continue;
+                }
+                if (runlen)
+                    w += (size_t)snprintf(where + w, sizeof where - w, "%s[step %llu: slots %u-%u kind %u]",
+                                          printed++ ? ", " : "", (unsigned long long)prev_step, run0, run0 + runlen - 1,
+                                          kind0);
+                if (i == R->nfail_logged) break;
+                prev_step = st_i;
+                run0 = slot;
+                runlen = 1;
+                kind0 = R->fail_kind[i];
+                (void)sn;
+            }
+        }
         if (R->rc) rc = R->rc;
         qsort(R->lat, R->nlat, sizeof(double), cmpd);
         const double p50 = R->nlat ? R->lat[R->nlat / 2] : 0.0, p99 = R->nlat ? R->lat[(R->nlat * 99) / 100] : 0.0;
@@ -463,9 +567,11 @@ int main(int argc, char** argv) {
         tx_full += R->tx_full;
         if ((nic ? R->wall : R->busy) > t_max) t_max = nic ? R->wall : R->busy;
         free(R->lat);
+        free(R->step_seq);
+        free(R->step_n);
     }
     printf("], \"mframes_s_total\": %.3f, \"frames\": %llu, \"checked\": %llu, \"tx_full\": %llu, \"failures\": %llu, "
-           "\"rc\": %d}\n", t_max > 0 ? 1e-6 * (double)tot / t_max : 0.0, (unsigned long long)tot,
-           (unsigned long long)checked, (unsigned long long)tx_full, (unsigned long long)fail, rc);
+           "\"where\": \"%s\", \"rc\": %d}\n", t_max > 0 ? 1e-6 * (double)tot / t_max : 0.0, (unsigned long long)tot,
+           (unsigned long long)checked, (unsigned long long)tx_full, (unsigned long long)fail, where, rc);
     return rc || fail ? 1 : 0;
 }

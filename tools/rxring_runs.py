@@ -34,13 +34,32 @@ RUNS = [
 ]
 
 
+# round 6: the runs that still failed with the split accounting (1024 x 1500-B steps, pipe depth 3-4, NIC thread),
+# and the variants that tell where the failures come from
+DIAG = [
+    ("lowlat", 1024, 1500, 3, [], None, None),
+    ("lowlat", 1024, 1500, 3, ["ring=4096", "groups=1"], None, None),
+    ("lowlat", 1024, 1500, 3, ["ring=4096", "huge=1"], None, None),
+    ("lowlat", 1024, 1500, 2, [], None, None),
+    ("lowlat", 1024, 1500, 0, [], None, None),
+    ("lowlat", 1024, 1500, 0, ["ring=4096", "queues=3"], None, None),
+    ("zerocopy", 1024, 1500, 3, [], None, None),
+    ("staged", 1024, 1500, 3, [], None, None),
+    ("lowlat", 1024, 1500, 3, ["ring=16384", "nic=burst"], None, None),
+    ("lowlat", 512, 1500, 3, [], None, None),
+    ("lowlat", 1024, 512, 3, [], None, None),
+    ("lowlat", 1024, 1500, 4, [], None, None),
+]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--diag", action="store_true", help="the round-6 diagnosis variants instead of the round-5 runs")
     args = ap.parse_args()
     exe = os.path.join(ROOT, "tools", "rxring")
     bad = 0
-    for mode, step, ln, pipe, extra, r5_rate, r5_fail in RUNS:
+    for mode, step, ln, pipe, extra, r5_rate, r5_fail in (DIAG if args.diag else RUNS):
         cmd = [exe, str(step), mode, str(args.seconds), f"len={ln}", "frames=16384", f"pipe={pipe}"] + \
             (extra or ["ring=4096"])
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
@@ -49,11 +68,13 @@ def main():
             d = json.loads(line)
         except json.JSONDecodeError:
             d = {"raw": line[-400:], "stderr": p.stderr[-400:]}
-        d["r5"] = {"mframes_s_total": r5_rate, "failures": r5_fail}
+        if r5_rate is not None:
+            d["r5"] = {"mframes_s_total": r5_rate, "failures": r5_fail}
         d["cmd"] = " ".join(["tools/rxring"] + cmd[1:])
         bad += int(d.get("failures", 1) != 0)
         print(json.dumps(d), flush=True)
-    print(json.dumps({"tool": "rxring_runs", "runs": len(RUNS), "runs_with_correctness_failures": bad}), flush=True)
+    print(json.dumps({"tool": "rxring_runs", "runs": len(DIAG if args.diag else RUNS),
+                      "runs_with_correctness_failures": bad}), flush=True)
     return 0
 
 
