@@ -320,7 +320,7 @@ def rx_loop(seconds=2.0):
             q = d["per_queue"][0]
             out[name] = {"mframes_per_s": q["mframes_s"], "us_per_step": q["us_per_step"], "p50_us": q["p50_us"],
                          "p99_us": q["p99_us"], "frames": d["frames"], "checked": d["checked"],
-                         "failures": d["failures"], "mode": q["mode"]}
+                         "failures": d["failures"], "tx_full": d.get("tx_full"), "mode": q["mode"]}
             if env:
                 out[name]["env"] = env
         except Exception as e:  # a measurement leg: report, never fail the bench line

@@ -215,7 +215,8 @@ enum xsk_gpu_mode {
  * With the runtime's default (GPU_MAX_HW_QUEUES unset or 4) that is 4; a deployment that sets GPU_MAX_HW_QUEUES=8 in
  * its environment gets 8 (round 5, tools/rxring: a depth-8 pipelined RX loop at 64-frame steps 44-45 Mframes/s against
  * 29-30 at depth 4).  Not more: with 16 resident kernels the grids were time-sliced (a depth-16 pipe
- * 0.12 Mframes/s), the device's hardware queue slots oversubscribed. */
+ * 0.12 Mframes/s), the device's hardware queue slots oversubscribed.  The cap in force is xsk_gpu_lowlat_cap(device);
+ * this constant is only its ceiling. */
 #define XSK_GPU_LOWLAT_PER_DEVICE 8
 
 /* Reserve `queues` (<= XSK_GPU_LOWLAT_PER_DEVICE) of `device`'s highest-priority hardware queues for the application's
@@ -223,6 +224,12 @@ enum xsk_gpu_mode {
  * Process-wide, host-only (no device call).  Returns the resident LOWLAT kernels now allowed on the device, or
  * -EINVAL. */
 int xsk_gpu_lowlat_reserve(int device, uint32_t queues);
+
+/* The resident LOWLAT kernels a process may run on `device` now: min(XSK_GPU_LOWLAT_PER_DEVICE,
+ * GPU_MAX_HW_QUEUES (4 when unset)) less the queues reserved above -- the number to size LOWLAT contexts or a LOWLAT
+ * pipe's depth by (XSK_GPU_LOWLAT_PER_DEVICE is only the ceiling).  Host-only, changes nothing; -EINVAL for a negative
+ * or out-of-range device index. */
+int xsk_gpu_lowlat_cap(int device);
 
 /* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
  * xsk_utils.c:132-135; its base must be page-aligned, -EINVAL otherwise).  The UMEM is registered with the HIP
@@ -390,7 +397,11 @@ struct xsk_gpu_rx_result {
  * Counters: rx_packets += received (:233), rx_bytes += sum(len) (:229), tx_packets / tx_bytes count
  * the frames actually submitted (:171-172 count successful sends).  The TX kick (sendto on the XSK
  * fd, :86) stays with the caller, which owns the socket.  Returns the number of frames received
- * (0 if the RX ring was empty) or a negative errno; `res` may be NULL. */
+ * (0 if the RX ring was empty) or a negative errno; `res` may be NULL.  On an error the batch's frames stay on the RX
+ * ring for a retry when every one of them is known untouched (nothing was posted or launched, or a LOWLAT batch timed
+ * out unserved); when some may have been transformed (a partly served batch whose launch path failed, a launch error,
+ * a LOWLAT kernel still running after its timeout) the batch is dropped instead -- released from the RX ring, every
+ * frame back to `pool`, none transmitted, res->received set -- since a retry could transform a frame twice. */
 int xsk_gpu_rx_step(xsk_gpu_ctx* ctx, struct xsk_gpu_ring* rx, struct xsk_gpu_ring* fill, struct xsk_gpu_ring* tx,
                     struct xsk_gpu_frame_pool* pool, uint32_t max_batch, struct xsk_gpu_stats* stats,
                     struct xsk_gpu_rx_result* res);
@@ -417,9 +428,11 @@ uint32_t xsk_gpu_tx_complete(struct xsk_gpu_ring* comp, struct xsk_gpu_frame_poo
  *   3. refill the fill ring from `pool` (as xsk_gpu_rx_step does, but on every call: frames freed by a step that
  *      received nothing must reach the fill ring too, or with batches in flight it could run dry).
  * Returns the frames completed by this call (not the frames received), or a negative errno.  A batch whose completion
- * fails stays the oldest in flight, and the next step or flush runs it again through its context (as a caller retries
- * a failed xsk_gpu_rx_step); the call returns the error when it handed no frame on, else its count (the error comes
- * back from a later call if the rerun fails too).  A failed submit leaves its frames on the RX ring.
+ * fails with every frame untouched stays the oldest in flight, and the next step or flush runs it again through its
+ * context (as a caller retries a failed xsk_gpu_rx_step); a batch that may be partly transformed is dropped (its
+ * frames back to `pool`, none transmitted) and the pipe moves on.  The call returns the error when it handed no frame
+ * on, else its count (the error comes back from a later call if the rerun fails too).  A failed submit leaves its
+ * frames on the RX ring, or drops them the same way when some may have been transformed.
  * xsk_gpu_rx_pipe_flush completes every batch in flight (an idle link, teardown); with a failure it stops there, so
  * call it until xsk_gpu_rx_pipe_inflight() is 0.  xsk_gpu_rx_pipe_fini waits for
  * batches still in flight and drops their results: flush first.  Single caller thread, like a context. */

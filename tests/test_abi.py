@@ -188,6 +188,12 @@ def test_multi_and_lowlat_validation_without_gpu():
     assert L.xsk_gpu_init(C.byref(h), 0, buf.ctypes.data, 64, 64, 3) == EINVAL
     assert L.xsk_gpu_multi_process(None, None, 0, None, None, None) == EINVAL
     assert L.xsk_gpu_multi_set_options(None, 1) == EINVAL
+    # the effective resident-kernel cap is a query: reserving queues lowers it, asking changes nothing
+    assert L.xsk_gpu_lowlat_cap(-1) == EINVAL
+    c0 = L.xsk_gpu_lowlat_cap(0)
+    assert 1 <= c0 <= X.LOWLAT_PER_DEVICE
+    assert L.xsk_gpu_lowlat_reserve(0, 1) == c0 - 1 == L.xsk_gpu_lowlat_cap(0) == X.lowlat_cap(0)
+    assert L.xsk_gpu_lowlat_reserve(0, 0) == c0 == L.xsk_gpu_lowlat_cap(0)
     L.xsk_gpu_multi_fini(None)
     # the pipelined RX loop: depth 1..XSK_GPU_RX_PIPE_MAX, a valid mode, an aligned UMEM; NULL objects
     assert L.xsk_gpu_rx_pipe_init(C.byref(h), 0, buf.ctypes.data, 64, 0, 2) == EINVAL

@@ -23,7 +23,7 @@ __all__ = [
     "LIB_PATH", "lib", "build_id", "XskGpuError", "DESC_DTYPE", "REC_DTYPE", "STATS_DTYPE", "VERDICTS",
     "TX_REPLY", "DROP_SHORT", "DROP_NOT_IPV4", "DROP_NOT_ICMP", "DROP_NOT_ECHO", "DROP_BAD_DESC",
     "echo_dev", "synth_dev", "rearm_dev", "stream_read_dev", "workspace_size", "EchoContext",
-    "MODE_ZEROCOPY", "MODE_STAGED", "MODE_LOWLAT", "LOWLAT_MAX", "MultiContext", "tune_lib", "lowlat_reserve", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
+    "MODE_ZEROCOPY", "MODE_STAGED", "MODE_LOWLAT", "LOWLAT_MAX", "MultiContext", "tune_lib", "lowlat_reserve", "lowlat_cap", "timing_enable", "timing_read", "Ring", "FramePool", "RxResult",
     "classify_dev", "XDP_DROP", "XDP_PASS", "XDP_REDIRECT", "DROP_BAD_IP", "DROP_BAD_CSUM",
     "OPT_STRICT_IPV4", "OPT_VLAN", "OPT_VERIFY_CSUM", "OPT_ALL", "F_IP_CSUM_OK", "F_ICMP_CSUM_OK", "F_VLAN",
     "F_IP_OPTIONS",
@@ -125,6 +125,7 @@ _SIGS = {
     "xsk_gpu__lowlat_tune": ([_P, C.c_uint32, C.c_uint32, C.c_uint32], C.c_int),
     "xsk_gpu_multi_fini": ([_P], None),
     "xsk_gpu_lowlat_reserve": ([C.c_int, C.c_uint32], C.c_int),
+    "xsk_gpu_lowlat_cap": ([C.c_int], C.c_int),
     "xsk_gpu__staged_stats": ([_P, C.POINTER(C.c_uint64)], C.c_int),
     "xsk_gpu__staged_noalias": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu__lowlat_outcomes": ([_P, C.POINTER(C.c_uint64)], C.c_int),
@@ -270,6 +271,15 @@ def lowlat_reserve(device: int, queues: int) -> int:
         raise XskGpuError("xsk_gpu_lowlat_reserve", rc)
     return rc
 
+
+
+def lowlat_cap(device: int = 0) -> int:
+    """xsk_gpu_lowlat_cap: the resident LOWLAT kernels this process may run on `device` now (min(8,
+    GPU_MAX_HW_QUEUES) less the reserved queues), without changing anything."""
+    rc = lib().xsk_gpu_lowlat_cap(device)
+    if rc < 0:
+        raise XskGpuError("xsk_gpu_lowlat_cap", rc)
+    return rc
 
 def timing_enable(on: bool = True) -> None:
     _check("xsk_gpu_timing_enable", lib().xsk_gpu_timing_enable(1 if on else 0))

@@ -140,6 +140,10 @@ int xsk_gpu_lowlat_reserve(int device, uint32_t queues) {
     atomic_store(&g_ll_reserved[device], (int)queues);
     return ll_cap(device);
 }
+int xsk_gpu_lowlat_cap(int device) {
+    if (device < 0 || device >= LL_MAX_DEV) return -EINVAL;
+    return ll_cap(device);
+}
 static void ll_slot_give(int device) {
     if (device >= 0 && device < LL_MAX_DEV) atomic_fetch_sub(&g_ll_slots[device], 1);
 }
