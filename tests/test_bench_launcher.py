@@ -266,12 +266,12 @@ def test_rx_loop_leg_parses_rxring_and_never_fails_the_line(tmp_path, monkeypatc
     (tmp_path / "tools").mkdir()
     exe = tmp_path / "tools" / "rxring"
     line = ('{"tool": "rxring", "per_queue": [{"mode": 2, "mframes_s": 28.7, "us_per_step": 4.2, "p50_us": 3.1, '
-            '"p99_us": 9.0}], "frames": 1000, "checked": 1000, "failures": 0, "rc": 0}')
+            '"p99_us": 9.0}], "frames": 1000, "checked": 1000, "tx_full": 0, "failures": 0, "rc": 0}')
     exe.write_text("#!/bin/sh\ncase \"$*\" in *1024*) echo nothing; exit 1;; esac\necho '" + line + "'\n")
     exe.chmod(0o755)
     r = bench.rx_loop(0.1)
     assert r["step64"] == {"mframes_per_s": 28.7, "us_per_step": 4.2, "p50_us": 3.1, "p99_us": 9.0, "frames": 1000,
-                           "checked": 1000, "failures": 0, "mode": 2}
+                           "checked": 1000, "failures": 0, "tx_full": 0, "mode": 2}
     assert r["step64_pipe4"]["mframes_per_s"] == 28.7
     assert "error" in r["step1024"]
     assert r["step64_pipe8_hwq8"]["env"] == {"GPU_MAX_HW_QUEUES": "8"}
