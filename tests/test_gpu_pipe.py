@@ -176,4 +176,4 @@ def test_eight_doorbell_channels_under_gpu_max_hw_queues_8():
     print(f"depth-8 pipe under GPU_MAX_HW_QUEUES=8: {q['mframes_s']} Mframes/s")
     assert q["mode"] == X.MODE_LOWLAT  # (the pipe's last context: all eight kept their slot)
     assert d["failures"] == 0 and d["checked"] == d["frames"] > 0 and q["rc"] == 0
-    assert q["lowlat_timeouts_all_partial_failed"] == [0, 0, 0]
+    assert q["lowlat_timeouts_all_partial_failed_late"] == [0, 0, 0, 0] and d["tx_full"] == 0
