@@ -16,6 +16,7 @@
 #   devptr              the device alias hipHostRegister gives a page-aligned UMEM against its host address
 #   spread              tools/wg_spread.py: the shipped c3 kernel's per-workgroup start / end spread (timing probe 10)
 #   overlap             tools/overlap.py: consecutive c3 batches on one stream vs alternating over 2 and 3 streams
+#   overlapprof         rocprofv3 --kernel-trace of tools/overlap.py (1 and 2 streams): each launch's own duration
 #   readbw              tools/readbw.py: read kernels over slab sizes, each fitted as rate + per-launch intercept
 #   prof:<config>       rocprofv3 --kernel-trace --stats of bench.py --config <config>
 cd "$GRAFT_REPO_ROOT" || exit 3
@@ -41,6 +42,7 @@ for s in "$@"; do
     spread) run spread 300 python tools/wg_spread.py --config c3 --variants 10 --rounds 3 || exit 1 ;;
     overlap) run overlap 300 python tools/overlap.py --config c3 --steps 20 --streams 1,2,3 || exit 1 ;;
     readbw) run readbw 400 python tools/readbw.py || exit 1 ;;
+    overlapprof) run overlapprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/overlapprof -o run -- python3 $GRAFT_REPO_ROOT/tools/overlap.py --config c3 --steps 20 --streams 1,2 --reps 2 || exit 1 ;;
     prof:*) c=${s#prof:}; run prof_$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_$c -o run -- python3 $GRAFT_REPO_ROOT/bench.py --config $c --steps 20 --warmup 5 --no-cpu || exit 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
