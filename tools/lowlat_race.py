@@ -23,7 +23,7 @@ def main():
     bad_total = 0
     for rep in range(reps):
         for want in (True, False):
-            work = umem.copy()
+            work = X.umem_copy(umem)  # page-aligned, as xsk_gpu_init requires
             vs, rs = [], []
             with X.EchoContext(work, 0, max_batch=batch, mode=X.MODE_LOWLAT) as ctx:
                 for i in range(0, n, batch):

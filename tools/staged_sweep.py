@@ -34,7 +34,7 @@ def main():
     prev = None
     for n in ns:
         d = np.ascontiguousarray(descs[:n])
-        work = umem.copy()
+        work = X.umem_copy(umem)  # page-aligned, as xsk_gpu_init requires
         ts = []
         with X.EchoContext(work, 0, max_batch=n, mode=X.MODE_STAGED) as ctx:
             v, _, _ = ctx.process(d, want_recs=False)  # warm
