@@ -69,6 +69,83 @@ def describe_diff(umem, work, ref, descs, v, diff, ctx=None):
     return " | ".join(out)
 
 
+def test_context_teardown_beside_a_resident_lowlat_grid():
+    """Round 6 (tools/fini_block.py, profiles/r06/fini_block.jsonl): the HIP runtime's hipFree, and hipHostFree /
+    hipHostUnregister of host memory a kernel has used, wait for every stream of the device -- another context's
+    resident LOWLAT grid included, which leaves its stream only when it stops or has been idle for 50 ms.  So a context
+    closed beside a LOWLAT context returns once that grid goes idle.  Checked here: (a) on one thread, with the other
+    context's grid resident but idle, a close of every mode returns within 0.5 s (the grid's 50-ms idle exit) and both
+    contexts stay exact; (b) beside a LOWLAT context kept busy on a second thread for 1.5 s, contexts of every mode are
+    created, used and closed: every batch of both is exact, nothing fails, and each close returns no later than 0.5 s
+    after the busy context stops -- a teardown waits, it never hangs."""
+    import threading
+    _dev()
+    umem = np.zeros(1024 * 2048, np.uint8)
+    descs = oracle.synth_batch(umem, 1024, 0, 2048, 0x5EEDE100, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    v_ref, _, _ = oracle.echo_batch(ref, descs)
+    work = X.umem_copy(umem)
+
+    def lifecycle(mode):
+        u = X.umem_copy(umem[:256 * 2048])
+        d = np.ascontiguousarray(descs[:64])
+        r = u.copy()
+        vr, _, _ = oracle.echo_batch(r, d)
+        ctx = X.EchoContext(u, 0, max_batch=64, mode=mode)
+        v, _, _ = ctx.process(d, want_recs=False)
+        t0 = time.perf_counter()
+        ctx.close()
+        t1 = time.perf_counter()
+        assert (v == vr).all() and (u == r).all()
+        return t1 - t0, t1
+
+    # (a) one thread, the other context's grid resident and idle
+    with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as a:
+        assert a.mode == X.MODE_LOWLAT
+        for mode in MODES:
+            work[:] = umem
+            v, _, _ = a.process(descs[:64], want_recs=False)  # the grid is resident again
+            assert (v == v_ref[:64]).all()
+            took, _ = lifecycle(mode)
+            assert took < 0.5, (mode, took)
+            v, _, _ = a.process(descs[64:128], want_recs=False)
+            assert (v == v_ref[64:128]).all() and (work[:128 * 2048] == ref[:128 * 2048]).all()
+
+    # (b) beside a context kept busy on a second thread
+    stop, errors, calls, busy_end = threading.Event(), [], [0], [None]
+
+    def busy():
+        try:
+            with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as c:
+                assert c.mode == X.MODE_LOWLAT
+                t_end = time.perf_counter() + 1.5
+                while not stop.is_set() and time.perf_counter() < t_end:
+                    work[:] = umem
+                    vs = [c.process(descs[i:i + 64], want_recs=False)[0] for i in range(0, len(descs), 64)]
+                    assert (np.concatenate(vs) == v_ref).all() and (work == ref).all()
+                    calls[0] += 1
+                busy_end[0] = time.perf_counter()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            busy_end[0] = time.perf_counter()
+            errors.append(repr(e))
+
+    th = threading.Thread(target=busy)
+    th.start()
+    time.sleep(0.2)
+    closes = []
+    try:
+        for mode in MODES:
+            closes.append((mode, *lifecycle(mode)))
+    finally:
+        stop.set()
+        th.join()
+    report = {"errors": errors, "busy_passes": calls[0],
+              "closes": [(m, round(t, 3), round(e - busy_end[0], 3)) for m, t, e in closes]}
+    assert not errors and calls[0] > 0, report
+    assert all(e < busy_end[0] + 0.5 for _, _, e in closes), report
+    print(f"closes beside a busy LOWLAT context: {report}")
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_host_umem_starts_on_a_page_of_its_own(mode):
     """two UMEMs carved from one allocation so that they share a page -- the layout round 5's numpy
