@@ -233,7 +233,12 @@ int xsk_gpu_lowlat_cap(int device);
 
 /* Bind a context to GPU `device` and the caller's UMEM (e.g. the posix_memalign'd buffer of
  * xsk_utils.c:132-135; its base must be page-aligned, -EINVAL otherwise).  The UMEM is registered with the HIP
- * runtime (hipHostRegister) until xsk_gpu_fini().  max_batch bounds n of later calls. */
+ * runtime (hipHostRegister, portable + mapped) until the last context, multi object or pipe over it is released:
+ * several of them may share one UMEM (AF_XDP sockets sharing a UMEM, one context per RX queue), and the library counts
+ * its users of each registration (the runtime keeps one per base and does not); a UMEM that is a part of one already
+ * registered by the library uses that registration.  -EBUSY for a UMEM that starts inside such a registration and
+ * runs past its end.  A UMEM the caller registered with the runtime itself is used as it is (it must be mapped) and
+ * stays registered.  max_batch bounds n of later calls. */
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode);
 
 /* The mode `ctx` runs in (XSK_GPU_MODE_*): the one it was created with, except a LOWLAT request beyond

@@ -23,13 +23,17 @@ hipError_t hipGetDeviceCount(int* n) {
     return hipSuccess;
 }
 hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidDevice; }
-hipError_t hipHostRegister(void* p, size_t n, unsigned int f) {
-    (void)p, (void)n, (void)f;
-    return hipSuccess;
+static int g_umem_refs; /* the pipe's references of the UMEM registration (xsk_gpu_host.c's table) */
+int xsk_gpu__umem_ref(void* base, uint64_t size, void** reg_base) {
+    (void)size;
+    *reg_base = base;
+    g_umem_refs++;
+    return 0;
 }
-hipError_t hipHostUnregister(void* p) {
-    (void)p;
-    return hipSuccess;
+void xsk_gpu__umem_unref(void* reg_base) {
+    if (!reg_base) return;
+    assert(g_umem_refs > 0);
+    g_umem_refs--;
 }
 hipError_t hipGetLastError(void) { return hipSuccess; }
 int xsk_gpu__dev_save(void) { return 0; }
@@ -360,6 +364,7 @@ int main(void) {
         xsk_gpu_rx_pipe_fini(p);
         g_ll_left = 1000;
     }
+    assert(g_umem_refs == 0); /* every pipe gave its registration reference back */
     printf("rx pipe ok\n");
     return 0;
 }

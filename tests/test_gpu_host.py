@@ -2,6 +2,7 @@
 (4096 x 64-B frames in one 16 MiB UMEM of 4 KiB chunks, RX_BATCH_SIZE batches -- src/lib/xsk_utils.h:6-8,
 src/lib/xsk_receive.c:220-233) in every host mode, the low-latency doorbell mode (resident polling kernel),
 and the multi-context path (several contexts over ONE UMEM, descriptor i on context i mod G)."""
+import ctypes
 import time
 
 import numpy as np
@@ -144,6 +145,88 @@ def test_context_teardown_beside_a_resident_lowlat_grid():
     assert not errors and calls[0] > 0, report
     assert all(e < busy_end[0] + 0.5 for _, _, e in closes), report
     print(f"closes beside a busy LOWLAT context: {report}")
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_contexts_sharing_one_umem(mode):
+    """Round 6 (tools/doublereg_probe.py, profiles/r06/doublereg.jsonl): the HIP runtime keeps ONE registration per base
+    address and counts nothing -- a second hipHostRegister of the base succeeds, the first hipHostUnregister removes it
+    for both -- so two contexts over one UMEM (AF_XDP sockets sharing a UMEM, one context per RX queue) broke when one
+    closed: the other's next batch failed with -EIO, in every mode.  The library now counts its users of a base
+    (xsk_gpu__umem_ref).  Checked: two contexts, a context over a part of the UMEM, a multi object and a pipe over one
+    UMEM serve their shares exactly; after any of them closes the others still serve exactly; a UMEM that starts inside
+    a registration and runs past its end gets -EBUSY; the last close releases the registration; a UMEM the caller
+    registered itself stays registered."""
+    _dev()
+    n = 2048
+    req = np.zeros(n * 4096, np.uint8)
+    descs = oracle.synth_batch(req, n, 0, 4096, 0x5EED5A4E + mode, mode=1, len_lo=20, len_hi=1500)
+    ref = req.copy()
+    v_ref, _, _ = oracle.echo_batch(ref, descs)
+    big = X.umem_zeros(2 * req.nbytes)
+    u = big[:req.nbytes]  # the same base as `big`, half its bytes
+    refs = lambda: X.lib().xsk_gpu__umem_refs(u.ctypes.data)  # noqa: E731
+
+    def serve(ctx, idx):
+        v, _, _ = ctx.process(np.ascontiguousarray(descs[idx]), want_recs=False)
+        assert (v == v_ref[idx]).all()
+
+    a = X.EchoContext(u, 0, max_batch=n, mode=mode)
+    b = X.EchoContext(u, 0, max_batch=n, mode=mode)
+    try:
+        assert refs() == 2
+        u[:] = req
+        serve(a, slice(0, n, 2))  # queue 0: even frames
+        serve(b, slice(1, n, 2))  # queue 1: odd frames
+        assert (u == ref).all()
+        with pytest.raises(X.XskGpuError, match="EBUSY"):  # more bytes than the registration of this base covers
+            X.EchoContext(big, 0, max_batch=64, mode=mode)
+        assert refs() == 2
+        b.close()
+        assert refs() == 1
+        u[:] = req
+        serve(a, slice(0, n))  # round 5's library: -EIO here
+        assert (u == ref).all()
+        half = n // 2  # a context over the second half of the UMEM: a reference of the same registration
+        dp = descs[half:].copy()
+        dp["addr"] -= half * 4096
+        with X.EchoContext(u[half * 4096:], 0, max_batch=n, mode=mode) as c:
+            assert refs() == 2
+            u[:] = req
+            v, _, _ = c.process(dp, want_recs=False)
+            assert (v == v_ref[half:]).all() and (u[half * 4096:] == ref[half * 4096:]).all()
+        assert refs() == 1
+        m = X.MultiContext(u, [0], max_batch=n, mode=mode)
+        p = X.RxPipe(u, 0, depth=2, mode=mode)
+        assert refs() == 3
+        u[:] = req
+        v, _, _ = m.process(descs, want_recs=False)
+        assert (v == v_ref).all() and (u == ref).all()
+        m.close()
+        p.close()
+        assert refs() == 1
+        u[:] = req
+        serve(a, slice(0, n))
+        assert (u == ref).all()
+    finally:
+        b.close()
+        a.close()
+    assert refs() == 0
+    # the registration is gone: the runtime no longer knows the base
+    hip = ctypes.CDLL("libamdhip64.so")
+    flags = ctypes.c_uint()
+    assert hip.hipHostGetFlags(ctypes.byref(flags), ctypes.c_void_p(u.ctypes.data)) != 0
+    hip.hipGetLastError()
+    # a UMEM the caller registered: used, and left registered at close
+    assert hip.hipHostRegister(ctypes.c_void_p(u.ctypes.data), ctypes.c_size_t(u.nbytes), 3) == 0
+    try:
+        with X.EchoContext(u, 0, max_batch=n, mode=mode) as c:
+            u[:] = req
+            serve(c, slice(0, n))
+            assert (u == ref).all()
+        assert refs() == 0
+    finally:
+        assert hip.hipHostUnregister(ctypes.c_void_p(u.ctypes.data)) == 0  # still the caller's
 
 
 @pytest.mark.parametrize("mode", MODES)

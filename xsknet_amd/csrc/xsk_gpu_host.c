@@ -29,6 +29,7 @@
 #define __HIP_PLATFORM_AMD__ 1
 #include <errno.h>
 #include <hip/hip_runtime_api.h>
+#include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
@@ -79,7 +80,7 @@ struct xsk_gpu_ctx {
     int stage_rec[2];       /* ... once one has */
     int stage_half;     /* the half the next host pack fills */
     uint64_t stage_bytes; /* bytes per half (STAGE_HALF; xsk_gpu__staged_noalias sets others for tests) */
-    int registered;   /* this context registered the UMEM (and unregisters it at fini) */
+    void* reg_base;   /* the registration this context holds a reference of (xsk_gpu__umem_ref), or NULL */
     xsk_gpu__lowlat* ll; /* LOWLAT: the doorbell channel */
     int ll_slot;         /* holds one of the device's XSK_GPU_LOWLAT_PER_DEVICE LOWLAT slots */
     uint64_t ll_outcome[4]; /* LOWLAT doorbell batches that missed their timeout: all, completed through the launch path
@@ -174,6 +175,95 @@ static int fail(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EIO
         }                                   \
     } while (0)
 
+/* Registrations of host UMEMs, shared in process (round 6).  The HIP runtime keeps one registration per base address
+ * and counts nothing: a second hipHostRegister of a registered base succeeds, and the first hipHostUnregister removes
+ * it for every user (tools/doublereg_probe.py, profiles/r06/doublereg.jsonl).  So two contexts over one UMEM -- AF_XDP
+ * sockets sharing a UMEM (XDP_SHARED_UMEM), one context per RX queue -- broke when either closed: the other's next
+ * batch failed with -EIO.  Every registration the library makes goes through this table: the first user of a base
+ * registers it (portable + mapped), later users of the same UMEM -- or of a part of it -- take a reference of that
+ * registration, the last one unregisters.  A UMEM that starts inside a registration and runs past its end gets
+ * -EBUSY.  A base the runtime already knows as host memory and that lies in none of the library's registrations (the
+ * caller registered it) is used and never unregistered here.  The lock is held across the
+ * runtime calls, so a concurrent user of the same base never sees it half registered or half released. */
+#define UMEM_REG_MAX 256
+static pthread_mutex_t g_reg_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+    void* base;
+    uint64_t size;
+    int refs;
+    int external; /* registered by the caller: never unregistered here */
+} g_reg[UMEM_REG_MAX];
+static int g_nreg;
+
+int xsk_gpu__umem_ref(void* base, uint64_t size, void** reg_base) {
+    int rc = 0;
+    *reg_base = NULL;
+    const uintptr_t lo = (uintptr_t)base, hi = lo + size;
+    pthread_mutex_lock(&g_reg_mu);
+    for (int i = 0; i < g_nreg; i++) {
+        const uintptr_t elo = (uintptr_t)g_reg[i].base, ehi = elo + g_reg[i].size;
+        if (elo <= lo && hi <= ehi) { /* the same UMEM, or a part of one the library registered */
+            g_reg[i].refs++;
+            *reg_base = g_reg[i].base;
+            goto out;
+        }
+        if (elo <= lo && lo < ehi) { /* starts inside a registration and runs past its end */
+            rc = -EBUSY;
+            goto out;
+        }
+    }
+    if (g_nreg == UMEM_REG_MAX) {
+        rc = -ENOMEM;
+        goto out;
+    }
+    /* a base the runtime already knows as host memory (it lies in none of the library's registrations): the caller
+     * registered it */
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof at);
+    const int external = hipPointerGetAttributes(&at, base) == hipSuccess && at.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    if (!external) {
+        const hipError_t e = hipHostRegister(base, size, hipHostRegisterPortable | hipHostRegisterMapped);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            rc = fail(e);
+            goto out;
+        }
+    }
+    g_reg[g_nreg].base = base;
+    g_reg[g_nreg].size = size;
+    g_reg[g_nreg].refs = 1;
+    g_reg[g_nreg].external = external;
+    g_nreg++;
+    *reg_base = base;
+out:
+    pthread_mutex_unlock(&g_reg_mu);
+    return rc;
+}
+
+void xsk_gpu__umem_unref(void* reg_base) {
+    if (!reg_base) return;
+    pthread_mutex_lock(&g_reg_mu);
+    for (int i = 0; i < g_nreg; i++)
+        if (g_reg[i].base == reg_base) {
+            if (--g_reg[i].refs == 0) {
+                if (!g_reg[i].external) (void)hipHostUnregister(reg_base);
+                g_reg[i] = g_reg[--g_nreg];
+            }
+            break;
+        }
+    pthread_mutex_unlock(&g_reg_mu);
+}
+
+int xsk_gpu__umem_refs(const void* base) {
+    int n = 0;
+    pthread_mutex_lock(&g_reg_mu);
+    for (int i = 0; i < g_nreg; i++)
+        if (g_reg[i].base == base) n = g_reg[i].refs;
+    pthread_mutex_unlock(&g_reg_mu);
+    return n;
+}
+
 /* the caller's current device, to put back on return: object lifecycles and per-call paths all select their own
  * device and leave the caller's thread as they found it */
 int xsk_gpu__dev_save(void) {
@@ -205,7 +295,7 @@ static void fini_impl(xsk_gpu_ctx* c) {
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamSynchronize(c->stream[s]);
     if (c->mode == XSK_GPU_MODE_STAGED && c->d_umem) (void)hipFree(c->d_umem);
-    if (c->registered) (void)hipHostUnregister(c->umem);
+    xsk_gpu__umem_unref(c->reg_base);
     (void)hipFree(c->d_descs);
     (void)hipFree(c->d_verdicts);
     (void)hipFree(c->d_recs);
@@ -266,8 +356,7 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
     TRY(hipSetDevice(device));
     for (int s = 0; s < NSTREAMS; s++) TRY(hipStreamCreateWithFlags(&c->stream[s], hipStreamNonBlocking));
     if (!prereg) { /* mapped in every mode: STAGED's gather kernel reads scattered frames through the alias */
-        TRY(hipHostRegister(umem, umem_size, hipHostRegisterMapped));
-        c->registered = 1;
+        if ((rc = xsk_gpu__umem_ref(umem, umem_size, &c->reg_base)) != 0) goto out;
     }
     if (zerocopy(c)) {
         TRY(hipHostGetDevicePointer((void**)&c->d_umem, umem, 0));

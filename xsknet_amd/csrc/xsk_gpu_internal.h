@@ -159,6 +159,13 @@ xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i);
  * without being processed (fault injection for the partial-failure semantics). */
 int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 
+/* xsk_gpu_host.c: the in-process registrations of host UMEMs -- one runtime registration per UMEM, counted (the runtime
+ * keeps one per base and does not count).  ref: 0 with *reg_base = the registration referenced (to unref at release),
+ * -EBUSY (the range starts inside a registration and runs past it), -ENOMEM or -EIO; unref(reg_base): the last
+ * reference unregisters (NULL: no-op).  umem_refs: the references of the registration at `base` (tests). */
+XSK_GPU__HIDDEN int xsk_gpu__umem_ref(void* base, uint64_t size, void** reg_base);
+XSK_GPU__HIDDEN void xsk_gpu__umem_unref(void* reg_base);
+int xsk_gpu__umem_refs(const void* base);
 /* xsk_gpu_host.c: xsk_gpu_init over a UMEM the caller has already registered with the HIP runtime
  * (portable + mapped, e.g. the one registration of a multi-GPU object): the context neither registers
  * nor unregisters it. */

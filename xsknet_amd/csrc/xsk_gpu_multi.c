@@ -40,7 +40,7 @@ struct xsk_gpu_multi {
     uint8_t* umem;
     uint64_t umem_size;
     uint32_t max_batch;
-    int registered;
+    void* reg_base; /* the UMEM registration this object holds a reference of */
     int reg_device;
     struct multi_worker w[XSK_GPU_MULTI_MAX];
     /* the current job, published under mu */
@@ -113,10 +113,10 @@ void xsk_gpu_multi_fini(xsk_gpu_multi* m) {
         free(w->verd);
         free(w->recs);
     }
-    if (m->registered) {
+    if (m->reg_base) {
         const int caller_dev = xsk_gpu__dev_save();
         (void)hipSetDevice(m->reg_device);
-        (void)hipHostUnregister(m->umem);
+        xsk_gpu__umem_unref(m->reg_base);
         xsk_gpu__dev_restore(caller_dev);
     }
     pthread_cond_destroy(&m->go);
@@ -149,14 +149,10 @@ int xsk_gpu_multi_init(xsk_gpu_multi** out, const int* devices, uint32_t ndev, v
     /* one registration of the caller's UMEM for every device (portable) with a device alias (mapped) */
     m->reg_device = devices[0];
     const int caller_dev = xsk_gpu__dev_save();
-    const int reg = hipSetDevice(devices[0]) == hipSuccess &&
-                    hipHostRegister(umem, umem_size, hipHostRegisterPortable | hipHostRegisterMapped) == hipSuccess;
+    /* (shared and counted with every other user of this UMEM: xsk_gpu__umem_ref) */
+    rc = hipSetDevice(devices[0]) == hipSuccess ? xsk_gpu__umem_ref(umem, umem_size, &m->reg_base) : -EIO;
     xsk_gpu__dev_restore(caller_dev);
-    if (!reg) {
-        rc = -EIO;
-        goto fail;
-    }
-    m->registered = 1;
+    if (rc) goto fail;
     const uint32_t cap = (max_batch + ndev - 1) / ndev;
     for (uint32_t g = 0; g < ndev; g++) {
         struct multi_worker* w = &m->w[g];

@@ -28,7 +28,7 @@ struct pipe_slot {
 struct xsk_gpu_rx_pipe {
     int device;
     uint8_t* umem;
-    int registered;
+    void* reg_base; /* the UMEM registration this object holds a reference of */
     uint32_t depth;
     uint32_t head;  /* slot of the oldest batch in flight */
     uint32_t count; /* batches in flight: slots head, head + 1, ... (mod depth) */
@@ -38,10 +38,10 @@ struct xsk_gpu_rx_pipe {
 void xsk_gpu_rx_pipe_fini(xsk_gpu_rx_pipe* p) {
     if (!p) return;
     for (uint32_t i = 0; i < p->depth; i++) xsk_gpu_fini(p->s[i].ctx); /* (waits for a batch still in flight) */
-    if (p->registered) {
+    if (p->reg_base) {
         const int caller_dev = xsk_gpu__dev_save();
         (void)hipSetDevice(p->device);
-        (void)hipHostUnregister(p->umem);
+        xsk_gpu__umem_unref(p->reg_base);
         xsk_gpu__dev_restore(caller_dev);
     }
     free(p);
@@ -62,14 +62,13 @@ int xsk_gpu_rx_pipe_init(xsk_gpu_rx_pipe** out, int device, void* umem, uint64_t
     int rc = 0;
     /* one registration of the UMEM, mapped, for every context of the pipe */
     const int caller_dev = xsk_gpu__dev_save();
-    const int reg = hipSetDevice(device) == hipSuccess && hipHostRegister(umem, umem_size, hipHostRegisterMapped) == hipSuccess;
-    if (!reg) (void)hipGetLastError();
+    /* (shared and counted with every other user of this UMEM: xsk_gpu__umem_ref) */
+    rc = hipSetDevice(device) == hipSuccess ? xsk_gpu__umem_ref(umem, umem_size, &p->reg_base) : -EIO;
     xsk_gpu__dev_restore(caller_dev);
-    if (!reg) {
+    if (rc) {
         free(p);
-        return -EIO;
+        return rc;
     }
-    p->registered = 1;
     uint32_t kept = depth;
     for (uint32_t i = 0; i < depth; i++) {
         rc = xsk_gpu__init_prereg(&p->s[i].ctx, device, umem, umem_size, XSK_GPU_RX_MAX_STEP, mode);
