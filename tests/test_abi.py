@@ -153,7 +153,7 @@ def test_tuning_code_is_not_in_the_product_library():
         assert sym not in prod, sym
     # the product exports the C ABI, plus the CU count the tuning library links against and the test / tool hooks
     # of xsk_gpu_internal.h (LOWLAT diagnostics and knobs, forced grid, multi fault injection and context handles,
-    # staged copy-in record and no-alias switch, the UMEM registration references)
+    # staged copy-in record and no-alias switch, the UMEM registration references, the kept buffers)
     exported = set(re.findall(r"\bT (\w+)", prod))
     assert exported - set(declared_functions()) <= {"xsk_gpu__num_cu", "xsk_gpu__lowlat_trace", "xsk_gpu__lowlat_tune",
                                                     "xsk_gpu__echo_dev_grid", "xsk_gpu__multi_inject",
@@ -161,7 +161,7 @@ def test_tuning_code_is_not_in_the_product_library():
                                                     "xsk_gpu__multi_ctx", "xsk_gpu__lowlat_outcomes",
                                                     "xsk_gpu__lowlat_test_width", "xsk_gpu__rx_pipe_ctx",
                                                     "xsk_gpu__lowlat_live", "xsk_gpu__umem_view",
-                                                    "xsk_gpu__umem_refs"}, \
+                                                    "xsk_gpu__umem_refs", "xsk_gpu__buf_kept"}, \
         exported - set(declared_functions())
     tune = subprocess.run(["nm", "-D", "--defined-only", X.TUNE_LIB_PATH], capture_output=True, text=True,
                           check=True).stdout

@@ -147,6 +147,69 @@ def test_context_teardown_beside_a_resident_lowlat_grid():
     print(f"closes beside a busy LOWLAT context: {report}")
 
 
+def test_queue_close_beside_a_busy_lowlat_queue_over_a_shared_umem():
+    """Round 6: two RX queues over one UMEM (XDP_SHARED_UMEM).  Queue 0's LOWLAT context is kept busy on a thread;
+    queue 1's contexts (every mode) are created, used and closed beside it.  The UMEM registration is shared
+    (xsk_gpu__umem_ref) and the closing context's buffers are kept for reuse while a resident grid runs
+    (xsk_gpu__buf_free), so no close calls a runtime free that waits for queue 0's grid: each returns within 0.25 s
+    while queue 0 is still busy, every batch of both queues is exact, and once queue 0 closes nothing is kept."""
+    import threading
+    _dev()
+    n, half = 1024, 1024 * 2048
+    req = np.zeros(2 * half, np.uint8)
+    d0 = oracle.synth_batch(req, n, 0, 2048, 0x5EEDE200, mode=1, len_lo=20, len_hi=1500)  # queue 0: first half
+    d1 = oracle.synth_batch(req, n, half, 2048, 0x5EEDE201, mode=1, len_lo=20, len_hi=1500)  # queue 1: second half
+    ref = req.copy()
+    v0, _, _ = oracle.echo_batch(ref, d0)
+    v1, _, _ = oracle.echo_batch(ref, d1)
+    work = X.umem_copy(req)
+    stop, ready, errors, calls, busy_end = threading.Event(), threading.Event(), [], [0], [None]
+
+    def busy():
+        try:
+            with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as c:
+                assert c.mode == X.MODE_LOWLAT
+                ready.set()
+                t_end = time.perf_counter() + 20.0
+                while not stop.is_set() and time.perf_counter() < t_end:
+                    work[:half] = req[:half]
+                    vs = [c.process(d0[i:i + 64], want_recs=False)[0] for i in range(0, n, 64)]
+                    assert (np.concatenate(vs) == v0).all() and (work[:half] == ref[:half]).all()
+                    calls[0] += 1
+                busy_end[0] = time.perf_counter()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            busy_end[0] = time.perf_counter()
+            errors.append(repr(e))
+            ready.set()
+
+    th = threading.Thread(target=busy)
+    th.start()
+    closes = []
+    try:
+        assert ready.wait(30)
+        time.sleep(0.2)
+        for rep in range(2):
+            for mode in MODES:
+                work[half:] = req[half:]
+                ctx = X.EchoContext(work, 0, max_batch=n, mode=mode)
+                v, _, _ = ctx.process(d1, want_recs=False)
+                t0 = time.perf_counter()
+                ctx.close()
+                closes.append((mode, round(time.perf_counter() - t0, 4)))
+                assert (v == v1).all() and (work[half:] == ref[half:]).all()
+        kept_while_busy = X.lib().xsk_gpu__buf_kept(0)
+        alive = th.is_alive()
+    finally:
+        stop.set()
+        th.join()
+    report = {"errors": errors, "busy_passes": calls[0], "closes": closes, "kept": kept_while_busy}
+    assert not errors and alive and calls[0] > 0, report
+    assert max(t for _, t in closes) < 0.25, report
+    assert kept_while_busy > 0, report
+    assert X.lib().xsk_gpu__buf_kept(0) == 0 and X.lib().xsk_gpu__umem_refs(work.ctypes.data) == 0, report
+    print(f"queue closes beside a busy LOWLAT queue: {report}")
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_contexts_sharing_one_umem(mode):
     """Round 6 (tools/doublereg_probe.py, profiles/r06/doublereg.jsonl): the HIP runtime keeps ONE registration per base

@@ -9,7 +9,9 @@ context.  This tool times, each beside a LOWLAT context that a second thread kee
 and the same with no resident grid.  A call that waits for every stream of the device returns only when the busy phase
 ends (`ended_beside_busy_grid`: false).  One JSON line per case.  Result (profiles/r06/fini_block.jsonl and
 fini_block_steps.txt): hipFree, and hipHostFree / hipHostUnregister of memory a kernel has used, wait; so every
-context's close waits (its UMEM unregistration), until the resident grid stops or idles 50 ms (its idle exit).
+context's close waits (its UMEM unregistration), until the resident grid stops or idles 50 ms (its idle exit) --
+unless the UMEM is shared with another context (its registration stays) and the buffers are kept for reuse while a
+grid runs, as the library does since round 6: `lifecycle over its UMEM's second half`.
 
     python tools/fini_block.py [--busy-seconds 3]
 """
@@ -90,9 +92,12 @@ def used_then_released(kind):
                                                                                                "rc": int(rc2)}}
 
 
-def lifecycle(mode):
-    u = X.umem_zeros(256 * 2048)
-    d = oracle.synth_batch(u, 64, 0, 2048, 0x5EEDF000 + mode, mode=1, len_lo=20, len_hi=1500)
+def lifecycle(mode, shared=None):
+    """init / process / fini of a context over a UMEM of its own, or over the second half of `shared` (the busy
+    context's UMEM: two RX queues on one UMEM)"""
+    u = X.umem_zeros(256 * 2048) if shared is None else shared
+    off = 0 if shared is None else shared.nbytes // 2
+    d = oracle.synth_batch(u, 64, off, 2048, 0x5EEDF000 + mode, mode=1, len_lo=20, len_hi=1500)
     t0 = time.perf_counter()
     c = X.EchoContext(u, 0, max_batch=64, mode=mode)
     t1 = time.perf_counter()
@@ -113,9 +118,9 @@ def main():
           flush=True)
     # each case beside a LOWLAT context kept busy on another thread (a fresh busy phase per case: a teardown that waits
     # for the device returns only when that phase ends, so the next case would no longer be measured beside a busy grid)
-    u = X.umem_zeros(2048 * 2048)
+    u = X.umem_zeros(2 * 2048 * 2048)  # the busy context serves the first half
     d = oracle.synth_batch(u, 2048, 0, 2048, 0x5EEDF100, mode=1, len_lo=20, len_hi=1500)
-    req = u.copy()
+    req = u[:u.nbytes // 2].copy()
 
     def beside_busy(fn):
         stop, calls, end = threading.Event(), [0], [None]
@@ -125,7 +130,7 @@ def main():
                 assert c.mode == X.MODE_LOWLAT
                 t_end = time.perf_counter() + args.busy_seconds
                 while not stop.is_set() and time.perf_counter() < t_end:
-                    u[:] = req
+                    u[:len(req)] = req
                     for i in range(0, len(d), 64):
                         c.process(d[i:i + 64], want_recs=False)
                         calls[0] += 1
@@ -145,6 +150,10 @@ def main():
     for m in (X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT):  # the library's own teardown ...
         print(json.dumps({"case": f"beside a busy LOWLAT context: mode{m} lifecycle", "busy_seconds": args.busy_seconds,
                           **beside_busy(lambda: lifecycle(m))}), flush=True)
+    for m in (X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT):  # ... over the busy context's UMEM (shared) ...
+        print(json.dumps({"case": f"beside a busy LOWLAT context: mode{m} lifecycle over its UMEM's second half",
+                          "busy_seconds": args.busy_seconds, **beside_busy(lambda: lifecycle(m, shared=u))}),
+              flush=True)
     for kind in ("hipHostFree", "hipHostUnregister"):  # host memory a kernel has read, released
         print(json.dumps({"case": f"beside a busy LOWLAT context: {kind} of host memory a kernel read",
                           "busy_seconds": args.busy_seconds, **beside_busy(lambda: used_then_released(kind))}),

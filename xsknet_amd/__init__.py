@@ -127,6 +127,7 @@ _SIGS = {
     "xsk_gpu_lowlat_reserve": ([C.c_int, C.c_uint32], C.c_int),
     "xsk_gpu_lowlat_cap": ([C.c_int], C.c_int),
     "xsk_gpu__umem_refs": ([_P], C.c_int),
+    "xsk_gpu__buf_kept": ([C.c_int], C.c_int),
     "xsk_gpu__staged_stats": ([_P, C.POINTER(C.c_uint64)], C.c_int),
     "xsk_gpu__staged_noalias": ([_P, C.c_uint32], C.c_int),
     "xsk_gpu__lowlat_outcomes": ([_P, C.POINTER(C.c_uint64)], C.c_int),

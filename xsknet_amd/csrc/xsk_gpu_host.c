@@ -58,6 +58,7 @@ struct xsk_gpu_ctx {
     struct xsk_gpu_rec* d_recs;
     struct xsk_gpu_stats* d_stats; /* [max_chunks] */
     void* d_ws[NSTREAMS];
+    size_t ws_size; /* bytes of each d_ws */
     uint8_t* d_pack;  /* STAGED: [max_batch][PACK] rewritten headers */
     uint8_t* h_pack;  /* STAGED: pinned host copy of d_pack */
     uint8_t* h_verd;  /* pinned (mapped) verdict staging */
@@ -147,6 +148,93 @@ int xsk_gpu_lowlat_cap(int device) {
 }
 static void ll_slot_give(int device) {
     if (device >= 0 && device < LL_MAX_DEV) atomic_fetch_sub(&g_ll_slots[device], 1);
+}
+
+/* Buffers of contexts and LOWLAT channels (round 6).  The HIP runtime's hipFree, and its hipHostFree of pinned memory a
+ * kernel has used, wait for every stream of the device -- another context's resident LOWLAT grid included, which
+ * leaves its stream only when it stops or has idled 50 ms (tools/fini_block.py, profiles/r06/fini_block.jsonl: 2.5 s
+ * beside a busy grid).  So a buffer released while any LOWLAT slot of its device is taken is kept here instead, for
+ * the next allocation of the same device, kind and size; kept buffers are freed once no slot of the device is taken
+ * (xsk_gpu__buf_free(d, 0, NULL, 0) at the end of every fini).  With the UMEM registration shared (xsk_gpu__umem_ref),
+ * closing one RX queue's context beside another queue's busy LOWLAT context then waits for nothing.  `kind`:
+ * XSK_GPU__BUF_DEV (hipMalloc) or XSK_GPU__BUF_HOST | hipHostMalloc flags.  A reused host buffer is zeroed as a fresh
+ * one's pages are; device buffers carry no such promise either way. */
+#define POOL_MAX 256
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct {
+    void* p;
+    size_t size;
+    int device;
+    unsigned kind;
+} g_pool[POOL_MAX];
+static int g_npool;
+
+static int ll_busy(int device) { return device >= 0 && device < LL_MAX_DEV && atomic_load(&g_ll_slots[device]) > 0; }
+
+static void buf_release(unsigned kind, void* p) {
+    if (kind & XSK_GPU__BUF_HOST)
+        (void)hipHostFree(p);
+    else
+        (void)hipFree(p);
+}
+
+int xsk_gpu__buf_alloc(int device, unsigned kind, void** p, size_t size) {
+    *p = NULL;
+    pthread_mutex_lock(&g_pool_mu);
+    for (int i = 0; i < g_npool; i++)
+        if (g_pool[i].device == device && g_pool[i].kind == kind && g_pool[i].size == size) {
+            *p = g_pool[i].p;
+            g_pool[i] = g_pool[--g_npool];
+            break;
+        }
+    pthread_mutex_unlock(&g_pool_mu);
+    if (*p) {
+        if (kind & XSK_GPU__BUF_HOST) memset(*p, 0, size);
+        return (int)hipSuccess;
+    }
+    return kind & XSK_GPU__BUF_HOST ? (int)hipHostMalloc(p, size, kind & ~XSK_GPU__BUF_HOST) : (int)hipMalloc(p, size);
+}
+
+void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size) {
+    struct {
+        void* p;
+        unsigned kind;
+    } drop[POOL_MAX + 1];
+    int ndrop = 0;
+    pthread_mutex_lock(&g_pool_mu);
+    if (!ll_busy(device)) { /* no resident grid: free it, and whatever was kept for this device */
+        for (int i = 0; i < g_npool;)
+            if (g_pool[i].device == device) {
+                drop[ndrop].p = g_pool[i].p;
+                drop[ndrop++].kind = g_pool[i].kind;
+                g_pool[i] = g_pool[--g_npool];
+            } else {
+                i++;
+            }
+        if (p) {
+            drop[ndrop].p = p;
+            drop[ndrop++].kind = kind;
+        }
+    } else if (p && g_npool < POOL_MAX) {
+        g_pool[g_npool].p = p;
+        g_pool[g_npool].size = size;
+        g_pool[g_npool].device = device;
+        g_pool[g_npool].kind = kind;
+        g_npool++;
+    } else if (p) { /* the pool is full: free it (and wait) */
+        drop[ndrop].p = p;
+        drop[ndrop++].kind = kind;
+    }
+    pthread_mutex_unlock(&g_pool_mu);
+    for (int i = 0; i < ndrop; i++) buf_release(drop[i].kind, drop[i].p);
+}
+
+int xsk_gpu__buf_kept(int device) {
+    int n = 0;
+    pthread_mutex_lock(&g_pool_mu);
+    for (int i = 0; i < g_npool; i++) n += g_pool[i].device == device;
+    pthread_mutex_unlock(&g_pool_mu);
+    return n;
 }
 
 /* STAGED: frames in the next chunk of an n-frame batch with `rem` frames left -- a batch of at most CHUNK_FRAMES is
@@ -294,22 +382,27 @@ static void fini_impl(xsk_gpu_ctx* c) {
     if (c->ll_slot) ll_slot_give(c->device); /* ... before its hardware queue is offered to another context */
     for (int s = 0; s < NSTREAMS; s++)
         if (c->stream[s]) (void)hipStreamSynchronize(c->stream[s]);
-    if (c->mode == XSK_GPU_MODE_STAGED && c->d_umem) (void)hipFree(c->d_umem);
+    const int d = c->device;
+    const size_t nd = (size_t)c->max_batch * sizeof(struct xsk_gpu_desc);
+    const size_t nst = (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats);
+    if (c->mode == XSK_GPU_MODE_STAGED && c->d_umem) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_umem, c->umem_size);
     xsk_gpu__umem_unref(c->reg_base);
-    (void)hipFree(c->d_descs);
-    (void)hipFree(c->d_verdicts);
-    (void)hipFree(c->d_recs);
-    (void)hipFree(c->d_stats);
-    for (int s = 0; s < NSTREAMS; s++) (void)hipFree(c->d_ws[s]);
-    (void)hipFree(c->d_pack);
-    (void)hipFree(c->d_stage);
-    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->d_descs) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_descs, nd);
+    if (c->d_verdicts) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_verdicts, c->max_batch);
+    if (c->d_recs) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_recs, (size_t)c->max_batch * sizeof(struct xsk_gpu_rec));
+    if (c->d_stats) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_stats, nst);
+    for (int s = 0; s < NSTREAMS; s++)
+        if (c->d_ws[s]) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_ws[s], c->ws_size);
+    if (c->d_pack) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_pack, (size_t)c->max_batch * PACK);
+    if (c->d_stage) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, c->d_stage, 2u * (size_t)c->stage_bytes);
+    if (c->h_stage) xsk_gpu__buf_free(d, XSK_GPU__BUF_HOST, c->h_stage, 2u * (size_t)c->stage_bytes);
     for (int h = 0; h < 2; h++)
         if (c->stage_ev[h]) (void)hipEventDestroy(c->stage_ev[h]);
-    if (c->h_pack) (void)hipHostFree(c->h_pack);
-    if (c->h_verd) (void)hipHostFree(c->h_verd);
-    if (c->h_stats) (void)hipHostFree(c->h_stats);
-    if (c->h_descs) (void)hipHostFree(c->h_descs);
+    if (c->h_pack) xsk_gpu__buf_free(d, XSK_GPU__BUF_HOST, c->h_pack, (size_t)c->max_batch * PACK);
+    if (c->h_verd) xsk_gpu__buf_free(d, XSK_GPU__BUF_HOST | hipHostMallocMapped, c->h_verd, c->max_batch);
+    if (c->h_stats) xsk_gpu__buf_free(d, XSK_GPU__BUF_HOST | hipHostMallocMapped, c->h_stats, nst);
+    if (c->h_descs) xsk_gpu__buf_free(d, XSK_GPU__BUF_HOST | (zerocopy(c) ? hipHostMallocMapped : 0u), c->h_descs, nd);
+    xsk_gpu__buf_free(d, 0, NULL, 0); /* (no resident grid left on the device: what was kept goes too) */
     if (c->done) {
         for (uint32_t i = 0; i < c->max_chunks; i++)
             if (c->done[i]) (void)hipEventDestroy(c->done[i]);
@@ -367,14 +460,16 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
             c->m_umem = NULL;
             (void)hipGetLastError();
         }
-        TRY(hipMalloc((void**)&c->d_umem, umem_size));
-        TRY(hipMalloc((void**)&c->d_pack, (size_t)max_batch * PACK));
-        TRY(hipHostMalloc((void**)&c->h_pack, (size_t)max_batch * PACK, hipHostMallocDefault));
+        TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, (void**)&c->d_umem, umem_size));
+        TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, (void**)&c->d_pack, (size_t)max_batch * PACK));
+        TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_HOST, (void**)&c->h_pack, (size_t)max_batch * PACK));
     }
-    TRY(hipMalloc((void**)&c->d_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc)));
-    TRY(hipMalloc((void**)&c->d_verdicts, max_batch));
-    TRY(hipMalloc((void**)&c->d_recs, (size_t)max_batch * sizeof(struct xsk_gpu_rec)));
-    TRY(hipMalloc((void**)&c->d_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats)));
+    const size_t nd = (size_t)max_batch * sizeof(struct xsk_gpu_desc);
+    const size_t nst = (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats);
+    TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, (void**)&c->d_descs, nd));
+    TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, (void**)&c->d_verdicts, max_batch));
+    TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, (void**)&c->d_recs, max_batch * sizeof(struct xsk_gpu_rec)));
+    TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, (void**)&c->d_stats, nst));
     {
         const uint32_t per = max_batch < CHUNK_FRAMES || zerocopy(c) ? max_batch : CHUNK_FRAMES;
         const size_t ws = xsk_gpu_workspace_size(device, per);
@@ -382,13 +477,14 @@ static int init_impl(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_si
             rc = -EIO;
             goto out;
         }
-        for (int s = 0; s < NSTREAMS; s++) TRY(hipMalloc(&c->d_ws[s], ws));
+        c->ws_size = ws;
+        for (int s = 0; s < NSTREAMS; s++) TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_DEV, &c->d_ws[s], ws));
     }
-    TRY(hipHostMalloc((void**)&c->h_verd, max_batch, hipHostMallocMapped));
-    TRY(hipHostMalloc((void**)&c->h_stats, (size_t)c->max_chunks * sizeof(struct xsk_gpu_stats), hipHostMallocMapped));
-    if (!zerocopy(c)) TRY(hipHostMalloc((void**)&c->h_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc), 0));
+    TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_HOST | hipHostMallocMapped, (void**)&c->h_verd, max_batch));
+    TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_HOST | hipHostMallocMapped, (void**)&c->h_stats, nst));
+    if (!zerocopy(c)) TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_HOST, (void**)&c->h_descs, nd));
     if (zerocopy(c)) {
-        TRY(hipHostMalloc((void**)&c->h_descs, (size_t)max_batch * sizeof(struct xsk_gpu_desc), hipHostMallocMapped));
+        TRY(xsk_gpu__buf_alloc(device, XSK_GPU__BUF_HOST | hipHostMallocMapped, (void**)&c->h_descs, nd));
         TRY(hipHostGetDevicePointer((void**)&c->m_descs, c->h_descs, 0));
         TRY(hipHostGetDevicePointer((void**)&c->m_verd, c->h_verd, 0));
         TRY(hipHostGetDevicePointer((void**)&c->m_stats, c->h_stats, 0));
@@ -507,14 +603,14 @@ static int stage_hostpack(xsk_gpu_ctx* c, const struct xsk_gpu_desc* d, const st
         uint8_t *hs = NULL, *ds = NULL;
         hipEvent_t ev[2] = {NULL, NULL};
         int rc = 0;
-        if (hipHostMalloc((void**)&hs, 2u * (size_t)half, hipHostMallocDefault) != hipSuccess ||
-            hipMalloc((void**)&ds, 2u * (size_t)half) != hipSuccess)
+        if (xsk_gpu__buf_alloc(c->device, XSK_GPU__BUF_HOST, (void**)&hs, 2u * (size_t)half) != hipSuccess ||
+            xsk_gpu__buf_alloc(c->device, XSK_GPU__BUF_DEV, (void**)&ds, 2u * (size_t)half) != hipSuccess)
             rc = -ENOMEM;
         for (int h = 0; h < 2 && !rc; h++)
             if (hipEventCreateWithFlags(&ev[h], hipEventDisableTiming) != hipSuccess) rc = -EIO;
         if (rc) {
-            if (hs) (void)hipHostFree(hs);
-            if (ds) (void)hipFree(ds);
+            if (hs) xsk_gpu__buf_free(c->device, XSK_GPU__BUF_HOST, hs, 2u * (size_t)half);
+            if (ds) xsk_gpu__buf_free(c->device, XSK_GPU__BUF_DEV, ds, 2u * (size_t)half);
             for (int h = 0; h < 2; h++)
                 if (ev[h]) (void)hipEventDestroy(ev[h]);
             return rc;

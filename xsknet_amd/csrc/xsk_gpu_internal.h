@@ -159,6 +159,16 @@ xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i);
  * without being processed (fault injection for the partial-failure semantics). */
 int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 
+/* xsk_gpu_host.c: device (XSK_GPU__BUF_DEV, hipMalloc) and pinned host (XSK_GPU__BUF_HOST | hipHostMalloc flags)
+ * buffers of contexts and LOWLAT channels.  A buffer released while a LOWLAT slot of its device is taken is kept for
+ * the next allocation of the same device, kind and size instead of freed (the runtime's free would wait for the
+ * resident grids); free(d, 0, NULL, 0) frees what is kept for `d` once no slot is taken.  alloc returns a hipError_t.
+ * buf_kept: buffers kept for `device` (tests). */
+#define XSK_GPU__BUF_DEV 0u
+#define XSK_GPU__BUF_HOST 0x80000000u
+XSK_GPU__HIDDEN int xsk_gpu__buf_alloc(int device, unsigned kind, void** p, size_t size);
+XSK_GPU__HIDDEN void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size);
+int xsk_gpu__buf_kept(int device);
 /* xsk_gpu_host.c: the in-process registrations of host UMEMs -- one runtime registration per UMEM, counted (the runtime
  * keeps one per base and does not count).  ref: 0 with *reg_base = the registration referenced (to unref at release),
  * -EBUSY (the range starts inside a registration and runs past it), -ENOMEM or -EIO; unref(reg_base): the last

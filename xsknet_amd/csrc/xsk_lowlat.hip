@@ -376,15 +376,24 @@ int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll) {
     return 1;
 }
 
+// the channel's pinned host buffers: fine-grained (coherent) and mapped, so no GPU cache ever holds a copy
+constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
+constexpr size_t kDescBytes = (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc);
+constexpr size_t kRecBytes = (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec);
+
 static void ll_free(xsk_gpu__lowlat* ll) {
     if (!ll) return;
     xsk_gpu__lowlat_stop(ll);
     if (ll->stream) (void)hipStreamDestroy(ll->stream);
-    if (ll->h_bell) (void)hipHostFree(ll->h_bell);
-    if (ll->d_diag) (void)hipFree(ll->d_diag);
-    if (ll->h_descs) (void)hipHostFree(ll->h_descs);
-    if (ll->h_verd) (void)hipHostFree(ll->h_verd);
-    if (ll->h_recs) (void)hipHostFree(ll->h_recs);
+    // kept for the next channel while another resident grid runs on the device (xsk_gpu__buf_free: the runtime's
+    // free would wait for that grid)
+    const int d = ll->device;
+    const unsigned kh = XSK_GPU__BUF_HOST | kHostFlags;
+    if (ll->h_bell) xsk_gpu__buf_free(d, kh, (void*)ll->h_bell, sizeof(xsk_gpu__bell));
+    if (ll->d_diag) xsk_gpu__buf_free(d, XSK_GPU__BUF_DEV, ll->d_diag, sizeof(xsk_gpu__lldiag));
+    if (ll->h_descs) xsk_gpu__buf_free(d, kh, ll->h_descs, kDescBytes);
+    if (ll->h_verd) xsk_gpu__buf_free(d, kh, ll->h_verd, XSK_GPU_LOWLAT_MAX);
+    if (ll->h_recs) xsk_gpu__buf_free(d, kh, ll->h_recs, kRecBytes);
     free(ll);
 }
 
@@ -399,7 +408,7 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     // rests on the stores' own acknowledgements (the wave waits for them before `done`) and not on the L2 write-back
     // of the release (a late completion once returned exact verdicts with wrong records while these two
     // were coarse-grained; tests/test_gpu_staged.py::test_lowlat_late_completion_deterministic)
-    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    const unsigned fl = XSK_GPU__BUF_HOST | kHostFlags;
 #define LL_TRY(expr)                         \
     do {                                     \
         const hipError_t e_ = (expr);        \
@@ -415,14 +424,14 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     int lo = 0, hi = 0;
     LL_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     LL_TRY(hipStreamCreateWithPriority(&ll->stream, hipStreamNonBlocking, hi));
-    LL_TRY(hipHostMalloc((void**)&ll->h_bell, sizeof(xsk_gpu__bell), fl));
+    LL_TRY((hipError_t)xsk_gpu__buf_alloc(ll->device, fl, (void**)&ll->h_bell, sizeof(xsk_gpu__bell)));
     // XSK_GPU_LOWLAT_MAX slots plus a copy of the first 64 (the second poll's); fine-grained like the doorbell: every
     // batch rewrites them, so no GPU cache should ever hold a copy (round 5: once in ~1 G frames a whole 256-frame slice
     // came back DROP -- profiles/r05/rxpipe_pages.jsonl -- and a slice served from stale descriptors would do exactly
     // that; not seen again in 0.9 G frames either way, profiles/r05/lowlat_slice_recheck.jsonl)
-    LL_TRY(hipHostMalloc((void**)&ll->h_descs, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc), fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX, fl));
-    LL_TRY(hipHostMalloc((void**)&ll->h_recs, (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_rec), fl));
+    LL_TRY((hipError_t)xsk_gpu__buf_alloc(ll->device, fl, (void**)&ll->h_descs, kDescBytes));
+    LL_TRY((hipError_t)xsk_gpu__buf_alloc(ll->device, fl, (void**)&ll->h_verd, XSK_GPU_LOWLAT_MAX));
+    LL_TRY((hipError_t)xsk_gpu__buf_alloc(ll->device, fl, (void**)&ll->h_recs, kRecBytes));
     memset((void*)ll->h_bell, 0, sizeof(xsk_gpu__bell));
     // the descriptor slots too: the leader takes a polled slot as this batch's when its `options` tag equals the
     // batch's seq, and a recycled allocation may still hold an earlier channel's slots tagged 1, 2, 3, ... -- the seqs
@@ -430,7 +439,8 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     // descriptors for its own (seen once the pipelined loop made channels come and go: wrong verdicts, frames
     // untouched).  Zeroed, a slot's tag is never a posted seq (seqs start at 1).
     memset((void*)ll->h_descs, 0, (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc));
-    LL_TRY(hipMalloc((void**)&ll->d_diag, sizeof(xsk_gpu__lldiag)));
+    LL_TRY((hipError_t)xsk_gpu__buf_alloc(ll->device, XSK_GPU__BUF_DEV, (void**)&ll->d_diag,
+                                          sizeof(xsk_gpu__lldiag)));
     LL_TRY(hipMemset(ll->d_diag, 0, sizeof(xsk_gpu__lldiag)));
     LowlatArgs& A = ll->args;
     LL_TRY(hipHostGetDevicePointer((void**)&A.bell, ll->h_bell, 0));
