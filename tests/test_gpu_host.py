@@ -210,6 +210,87 @@ def test_queue_close_beside_a_busy_lowlat_queue_over_a_shared_umem():
     print(f"queue closes beside a busy LOWLAT queue: {report}")
 
 
+def test_context_churn_on_threads():
+    """Round 6: the shared registrations (xsk_gpu__umem_ref) and the kept buffers (xsk_gpu__buf_alloc) under concurrent
+    use.  For 3 s, on four threads: (0) a LOWLAT context serves quarter 0 of one UMEM; (1) contexts of every mode are
+    created over quarter 1 of the same UMEM, serve one batch and close; (2) the same over quarter 2 with multi objects
+    and pipes; (3) contexts over fresh page-aligned UMEMs of their own.  Every batch is exact, nothing fails, and at
+    the end no registration reference and no kept buffer is left."""
+    import threading
+    _dev()
+    n, q = 256, 256 * 2048
+    req = np.zeros(4 * q, np.uint8)
+    ds = [oracle.synth_batch(req, n, k * q, 2048, 0x5EEDC400 + k, mode=1, len_lo=20, len_hi=1500) for k in range(4)]
+    ref = req.copy()
+    vs = [oracle.echo_batch(ref, d)[0] for d in ds]
+    work = X.umem_copy(req)
+    stop, errors, counts = threading.Event(), [], [0, 0, 0, 0]
+
+    def part(k):
+        return slice(k * q, (k + 1) * q)
+
+    def served(k, v):
+        assert (v == vs[k]).all() and (work[part(k)] == ref[part(k)]).all(), k
+
+    def t0():
+        with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as c:
+            while not stop.is_set():
+                work[part(0)] = req[part(0)]
+                served(0, np.concatenate([c.process(ds[0][i:i + 64], want_recs=False)[0] for i in range(0, n, 64)]))
+                counts[0] += 1
+
+    def t1():
+        while not stop.is_set():
+            for mode in MODES:
+                work[part(1)] = req[part(1)]
+                with X.EchoContext(work, 0, max_batch=n, mode=mode) as c:
+                    served(1, c.process(ds[1], want_recs=False)[0])
+                counts[1] += 1
+
+    def t2():
+        while not stop.is_set():
+            for mode in MODES:
+                work[part(2)] = req[part(2)]
+                m = X.MultiContext(work, [0, 0], max_batch=n, mode=mode)
+                try:
+                    served(2, m.process(ds[2], want_recs=False)[0])
+                finally:
+                    m.close()
+                X.RxPipe(work, 0, depth=2, mode=mode).close()
+                counts[2] += 1
+
+    def t3():
+        own = req[part(3)]
+        d = ds[3].copy()
+        d["addr"] -= 3 * q
+        while not stop.is_set():
+            for mode in MODES:
+                u = X.umem_copy(own)
+                with X.EchoContext(u, 0, max_batch=n, mode=mode) as c:
+                    v = c.process(d, want_recs=False)[0]
+                assert (v == vs[3]).all() and (u == ref[part(3)]).all()
+                counts[3] += 1
+
+    def run(fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(f"{fn.__name__}: {e!r}")
+            stop.set()
+
+    ths = [threading.Thread(target=run, args=(f,)) for f in (t0, t1, t2, t3)]
+    for th in ths:
+        th.start()
+    time.sleep(3.0)
+    stop.set()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    assert min(counts) > 0, counts
+    assert X.lib().xsk_gpu__umem_refs(work.ctypes.data) == 0 and X.lib().xsk_gpu__buf_kept(0) == 0
+    print(f"churn: passes per thread {counts}")
+
+
 @pytest.mark.parametrize("mode", MODES)
 def test_contexts_sharing_one_umem(mode):
     """Round 6 (tools/doublereg_probe.py, profiles/r06/doublereg.jsonl): the HIP runtime keeps ONE registration per base
