@@ -293,11 +293,12 @@ def test_context_churn_on_threads():
 
 @pytest.mark.parametrize("mode", MODES)
 def test_contexts_sharing_one_umem(mode):
-    """Round 6 (tools/doublereg_probe.py, profiles/r06/doublereg.jsonl): the HIP runtime keeps ONE registration per base
-    address and counts nothing -- a second hipHostRegister of the base succeeds, the first hipHostUnregister removes it
-    for both -- so two contexts over one UMEM (AF_XDP sockets sharing a UMEM, one context per RX queue) broke when one
-    closed: the other's next batch failed with -EIO, in every mode.  The library now counts its users of a base
-    (xsk_gpu__umem_ref).  Checked: two contexts, a context over a part of the UMEM, a multi object and a pipe over one
+    """Round 6 (tools/doublereg_probe.py, profiles/r06/doublereg_attributes.jsonl): the HIP runtime keeps ONE registration
+    per base address and counts nothing -- a second hipHostRegister of the base succeeds, the first hipHostUnregister
+    removes it for both -- so when one of two contexts over one UMEM (AF_XDP sockets sharing a UMEM, one context per RX
+    queue) closed, the other went on over a UMEM the runtime no longer held registered, and a UMEM the caller had
+    registered itself lost its registration at the library's close.  The library now counts its users of each
+    registration (xsk_gpu__umem_ref).  Checked: two contexts, a context over a part of the UMEM, a multi object and a pipe over one
     UMEM serve their shares exactly; after any of them closes the others still serve exactly; a UMEM that starts inside
     a registration and runs past its end gets -EBUSY; the last close releases the registration; a UMEM the caller
     registered itself stays registered."""

@@ -53,6 +53,7 @@ def main():
     unreg(base)
     out["attributes: after unregister"] = attr(base)
     print(json.dumps({"case": "hipHostRegister", **out}), flush=True)
+    hip.hipGetLastError()  # (the deliberate 713 above would otherwise be the next launch check's "error")
     res = {}
     for m in (X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT):
         a = X.EchoContext(u, 0, max_batch=64, mode=m)
@@ -66,6 +67,8 @@ def main():
     print(json.dumps({"case": "xsk_gpu_init twice over one UMEM", **res}), flush=True)
     if "--after-close" in sys.argv:
         after_close(u)
+    if "--unregistered-under" in sys.argv:
+        unregistered_under(u)
 
 
 def after_close(u):
@@ -93,6 +96,41 @@ def after_close(u):
             r["error"] = str(e)
         a.close()
         print(json.dumps({"case": f"mode{m}: A and B over one UMEM, B closed, A serves 2048 frames", **r}), flush=True)
+
+
+
+def unregistered_under(u):
+    """What round 5's library did after the second of two contexts over one UMEM closed: the runtime registration gone
+    (one raw hipHostUnregister) under a live context, which then serves 2048 frames.  Every verdict and frame against
+    the oracle; a wrong frame is matched against the other frames' replies."""
+    import numpy as np
+    import oracle
+    umem = np.zeros(u.nbytes, np.uint8)
+    descs = oracle.synth_batch(umem, 2048, 0, 4096, 0x5EEDD0B2, mode=1, len_lo=20, len_hi=1500)
+    ref = umem.copy()
+    v_ref, _, _ = oracle.echo_batch(ref, descs)
+    for m in (X.MODE_ZEROCOPY, X.MODE_STAGED, X.MODE_LOWLAT):
+        r = {}
+        u[:] = umem
+        a = X.EchoContext(u, 0, max_batch=2048, mode=m)
+        hip.hipGetLastError()
+        r["raw_unregister"] = int(hip.hipHostUnregister(P(u.ctypes.data)))
+        hip.hipGetLastError()
+        try:
+            v, _, _ = a.process(descs, want_recs=False)
+            r["verdicts_exact"] = bool((v == v_ref).all())
+            rows = (u != ref).reshape(-1, 4096).any(axis=1)
+            bad = np.nonzero(rows)[0]
+            r["wrong_frames"] = int(len(bad))
+            r["untouched_frames"] = int(sum((u[i * 4096:(i + 1) * 4096] == umem[i * 4096:(i + 1) * 4096]).all()
+                                            for i in bad))
+            r["first_wrong"] = bad[:8].tolist()
+        except X.XskGpuError as e:
+            r["error"] = str(e)
+        hip.hipGetLastError()
+        a.close()
+        hip.hipGetLastError()
+        print(json.dumps({"case": f"mode{m}: registration removed under a live context, 2048 frames", **r}), flush=True)
 
 
 if __name__ == "__main__":
