@@ -160,7 +160,9 @@ static void ll_slot_give(int device) {
  * XSK_GPU__BUF_DEV (hipMalloc) or XSK_GPU__BUF_HOST | hipHostMalloc flags.  A reused host buffer is zeroed as a fresh
  * one's pages are; device buffers carry no such promise either way. */
 #define POOL_MAX 256
+#define POOL_BYTES_MAX (8ull << 30) /* kept at most, over every device and kind (a STAGED mirror is the UMEM's size) */
 static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static uint64_t g_pool_bytes;
 static struct {
     void* p;
     size_t size;
@@ -184,6 +186,7 @@ int xsk_gpu__buf_alloc(int device, unsigned kind, void** p, size_t size) {
     for (int i = 0; i < g_npool; i++)
         if (g_pool[i].device == device && g_pool[i].kind == kind && g_pool[i].size == size) {
             *p = g_pool[i].p;
+            g_pool_bytes -= size;
             g_pool[i] = g_pool[--g_npool];
             break;
         }
@@ -207,6 +210,7 @@ void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size) {
             if (g_pool[i].device == device) {
                 drop[ndrop].p = g_pool[i].p;
                 drop[ndrop++].kind = g_pool[i].kind;
+                g_pool_bytes -= g_pool[i].size;
                 g_pool[i] = g_pool[--g_npool];
             } else {
                 i++;
@@ -215,13 +219,14 @@ void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size) {
             drop[ndrop].p = p;
             drop[ndrop++].kind = kind;
         }
-    } else if (p && g_npool < POOL_MAX) {
+    } else if (p && g_npool < POOL_MAX && g_pool_bytes + size <= POOL_BYTES_MAX) {
+        g_pool_bytes += size;
         g_pool[g_npool].p = p;
         g_pool[g_npool].size = size;
         g_pool[g_npool].device = device;
         g_pool[g_npool].kind = kind;
         g_npool++;
-    } else if (p) { /* the pool is full: free it (and wait) */
+    } else if (p) { /* the pool is full (entries or bytes): free it (and wait) */
         drop[ndrop].p = p;
         drop[ndrop++].kind = kind;
     }

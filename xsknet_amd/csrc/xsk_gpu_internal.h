@@ -162,7 +162,8 @@ int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 /* xsk_gpu_host.c: device (XSK_GPU__BUF_DEV, hipMalloc) and pinned host (XSK_GPU__BUF_HOST | hipHostMalloc flags)
  * buffers of contexts and LOWLAT channels.  A buffer released while a LOWLAT slot of its device is taken is kept for
  * the next allocation of the same device, kind and size instead of freed (the runtime's free would wait for the
- * resident grids); free(d, 0, NULL, 0) frees what is kept for `d` once no slot is taken.  alloc returns a hipError_t.
+ * resident grids), up to 256 buffers and 8 GiB; free(d, 0, NULL, 0) frees what is kept for `d` once no slot is
+ * taken.  alloc returns a hipError_t.
  * buf_kept: buffers kept for `device` (tests). */
 #define XSK_GPU__BUF_DEV 0u
 #define XSK_GPU__BUF_HOST 0x80000000u
