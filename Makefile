@@ -23,7 +23,7 @@ HDRS     := $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip
 # (the device code and its launch: not include/xsk_gpu.h, whose comments change more often than its structs)
 BUILD_ID := $(shell cat $(CSRC)/xsk_echo.hip $(CSRC)/xsk_echo_device.h $(CSRC)/xsk_echo_kernels.h $(CSRC)/xsk_hip_util.h | sha256sum | cut -c1-16)-$(shell echo '$(HIPFLAGS)' | sha256sum | cut -c1-4)
 HIPOBJ   := $(CSRC)/xsk_echo.o $(CSRC)/xsk_aux.o $(CSRC)/xsk_classify.o $(CSRC)/xsk_lowlat.o
-HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o $(CSRC)/xsk_gpu_pipe.o $(CSRC)/xsk_gpu_umem.o
+HOSTOBJ  := $(CSRC)/xsk_gpu_host.o $(CSRC)/xsk_gpu_mem.o $(CSRC)/xsk_gpu_rx.o $(CSRC)/xsk_gpu_multi.o $(CSRC)/xsk_gpu_pipe.o $(CSRC)/xsk_gpu_umem.o
 TUNEOBJ  := $(CSRC)/tune/xsk_tune_product.o
 
 $(CSRC)/%.o: $(CSRC)/%.hip $(HDRS)

@@ -159,7 +159,9 @@ xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i);
  * without being processed (fault injection for the partial-failure semantics). */
 int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 
-/* xsk_gpu_host.c: device (XSK_GPU__BUF_DEV, hipMalloc) and pinned host (XSK_GPU__BUF_HOST | hipHostMalloc flags)
+/* xsk_gpu_host.c: 1 while a LOWLAT slot of `device` is taken (a resident grid may run there). */
+XSK_GPU__HIDDEN int xsk_gpu__ll_busy(int device);
+/* xsk_gpu_mem.c: device (XSK_GPU__BUF_DEV, hipMalloc) and pinned host (XSK_GPU__BUF_HOST | hipHostMalloc flags)
  * buffers of contexts and LOWLAT channels.  A buffer released while a LOWLAT slot of its device is taken is kept for
  * the next allocation of the same device, kind and size instead of freed (the runtime's free would wait for the
  * resident grids), up to 256 buffers and 8 GiB; free(d, 0, NULL, 0) frees what is kept for `d` once no slot is
@@ -170,7 +172,7 @@ int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 XSK_GPU__HIDDEN int xsk_gpu__buf_alloc(int device, unsigned kind, void** p, size_t size);
 XSK_GPU__HIDDEN void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size);
 int xsk_gpu__buf_kept(int device);
-/* xsk_gpu_host.c: the in-process registrations of host UMEMs -- one runtime registration per UMEM, counted (the runtime
+/* xsk_gpu_mem.c: the in-process registrations of host UMEMs -- one runtime registration per UMEM, counted (the runtime
  * keeps one per base and does not count).  ref: 0 with *reg_base = the registration referenced (to unref at release),
  * -EBUSY (the range starts inside a registration and runs past it), -ENOMEM or -EIO; unref(reg_base): the last
  * reference unregisters (NULL: no-op).  umem_refs: the references of the registration at `base` (tests). */
