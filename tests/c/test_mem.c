@@ -95,6 +95,15 @@ hipError_t hipHostFree(void* p) {
     return hipSuccess;
 }
 
+static atomic_int g_yield_requests, g_yield_max;
+void xsk_gpu__ll_yield_all(int delta) {
+    const int v = atomic_fetch_add(&g_yield_requests, delta) + delta;
+    assert(v >= 0);
+    int m = atomic_load(&g_yield_max);
+    while (v > m && !atomic_compare_exchange_weak(&g_yield_max, &m, v)) {
+    }
+}
+
 static atomic_int g_busy[4];
 int xsk_gpu__ll_busy(int device) { return atomic_load(&g_busy[device]); }
 
@@ -115,6 +124,7 @@ static void test_registrations(void) {
     assert(rt_covers(u, sizeof u) && rt_unregisters == u0); /* still one user */
     xsk_gpu__umem_unref(rb);
     assert(!rt_covers(u, 1) && rt_unregisters == u0 + 1 && xsk_gpu__umem_refs(u) == 0);
+    assert(g_yield_requests == 0 && g_yield_max == 1); /* grids asked to yield around the unregistration only */
     xsk_gpu__umem_unref(NULL); /* no-op */
 
     /* a caller's own registration: used, left registered */

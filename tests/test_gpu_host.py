@@ -73,12 +73,13 @@ def describe_diff(umem, work, ref, descs, v, diff, ctx=None):
 def test_context_teardown_beside_a_resident_lowlat_grid():
     """Round 6 (tools/fini_block.py, profiles/r06/fini_block.jsonl): the HIP runtime's hipFree, and hipHostFree /
     hipHostUnregister of host memory a kernel has used, wait for every stream of the device -- another context's
-    resident LOWLAT grid included, which leaves its stream only when it stops or has been idle for 50 ms.  So a context
-    closed beside a LOWLAT context returns once that grid goes idle.  Checked here: (a) on one thread, with the other
-    context's grid resident but idle, a close of every mode returns within 0.5 s (the grid's 50-ms idle exit) and both
-    contexts stay exact; (b) beside a LOWLAT context kept busy on a second thread for 1.5 s, contexts of every mode are
-    created, used and closed: every batch of both is exact, nothing fails, and each close returns no later than 0.5 s
-    after the busy context stops -- a teardown waits, it never hangs."""
+    resident LOWLAT grid included, which leaves its stream only when it stops or has been idle for 50 ms.  A context
+    over a UMEM of its own unregisters it at close; the library then asks every resident grid to leave once idle (the
+    yield word, xsk_gpu__ll_yield_all) and keeps released buffers for reuse (xsk_gpu__buf_free), so the close does not
+    wait for the other context to go idle.  Checked here: (a) on one thread, with the other context's grid resident but
+    idle, a close of every mode returns within 0.5 s and both contexts stay exact; (b) beside a LOWLAT context kept busy
+    on a second thread, contexts of every mode over UMEMs of their own are created, used and closed: every batch of
+    both is exact, nothing fails, and every close returns within 0.25 s while the busy context is still serving."""
     import threading
     _dev()
     umem = np.zeros(1024 * 2048, np.uint8)
@@ -119,7 +120,7 @@ def test_context_teardown_beside_a_resident_lowlat_grid():
         try:
             with X.EchoContext(work, 0, max_batch=64, mode=X.MODE_LOWLAT) as c:
                 assert c.mode == X.MODE_LOWLAT
-                t_end = time.perf_counter() + 1.5
+                t_end = time.perf_counter() + 20.0
                 while not stop.is_set() and time.perf_counter() < t_end:
                     work[:] = umem
                     vs = [c.process(descs[i:i + 64], want_recs=False)[0] for i in range(0, len(descs), 64)]
@@ -143,7 +144,8 @@ def test_context_teardown_beside_a_resident_lowlat_grid():
     report = {"errors": errors, "busy_passes": calls[0],
               "closes": [(m, round(t, 3), round(e - busy_end[0], 3)) for m, t, e in closes]}
     assert not errors and calls[0] > 0, report
-    assert all(e < busy_end[0] + 0.5 for _, _, e in closes), report
+    assert all(e < busy_end[0] for _, _, e in closes), report  # closed while the other context served
+    assert max(t for _, t, _ in closes) < 0.25, report
     print(f"closes beside a busy LOWLAT context: {report}")
 
 

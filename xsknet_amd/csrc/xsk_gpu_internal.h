@@ -159,6 +159,9 @@ xsk_gpu_ctx* xsk_gpu__rx_pipe_ctx(xsk_gpu_rx_pipe* p, uint32_t i);
  * without being processed (fault injection for the partial-failure semantics). */
 int xsk_gpu__multi_inject(xsk_gpu_multi* m, uint32_t g, int rc);
 
+/* xsk_lowlat.hip: ask every resident LOWLAT grid of the process to leave once idle (delta +1), or stop asking (-1);
+ * requests count.  Used around a runtime call that waits for every stream of the device (hipHostUnregister). */
+XSK_GPU__HIDDEN void xsk_gpu__ll_yield_all(int delta);
 /* xsk_gpu_host.c: 1 while a LOWLAT slot of `device` is taken (a resident grid may run there). */
 XSK_GPU__HIDDEN int xsk_gpu__ll_busy(int device);
 /* xsk_gpu_mem.c: device (XSK_GPU__BUF_DEV, hipMalloc) and pinned host (XSK_GPU__BUF_HOST | hipHostMalloc flags)

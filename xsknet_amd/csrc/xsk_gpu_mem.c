@@ -86,7 +86,13 @@ void xsk_gpu__umem_unref(void* reg_base) {
     for (int i = 0; i < g_nreg; i++)
         if (g_reg[i].base == reg_base) {
             if (--g_reg[i].refs == 0) {
-                if (!g_reg[i].external) (void)hipHostUnregister(reg_base);
+                if (!g_reg[i].external) {
+                    /* the runtime waits here for every stream of the device: resident LOWLAT grids are asked to
+                     * leave once idle (their next batch relaunches them) instead of being waited out */
+                    xsk_gpu__ll_yield_all(+1);
+                    (void)hipHostUnregister(reg_base);
+                    xsk_gpu__ll_yield_all(-1);
+                }
                 g_reg[i] = g_reg[--g_nreg];
             }
             break;

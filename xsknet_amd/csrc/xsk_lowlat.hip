@@ -30,6 +30,7 @@
 // so no slice is served twice.  The exit path is Dekker-safe: the leader clears `alive`, then looks at the
 // doorbell once more and resumes if a batch slipped in.
 #include <errno.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -43,6 +44,7 @@ using namespace xskgpu;
 namespace {
 
 constexpr uint64_t kIdleTicks = 5000000ull;  // 50 ms at 100 MHz (s_memrealtime)
+constexpr uint64_t kYieldTicks = 4000ull;    // the leader looks at its device's yield word every 40 us while idle
 constexpr int kLLTPW = 1;                    // 16 tiles = 1024 frames per doorbell, one round
 constexpr int kLLSync = 0;                   // one round: write as soon as the wave has read
 
@@ -62,6 +64,7 @@ struct LowlatArgs {
     xsk_gpu_rec* recs;
     uint32_t opts;
     uint32_t gen;  // launch generation (the leader's exit flag names it)
+    const uint32_t* yield;  // device alias of the device's yield word (xsk_gpu__ll_yield_all): nonzero -> leave
 };
 
 __device__ __forceinline__ uint32_t ld_sys(const volatile uint32_t* p) {
@@ -79,6 +82,7 @@ struct PollState {
     uint32_t served;
     uint64_t cA, aA, bA, cB, aB, bB;  // the two polls' registers: they stay live across the body
     uint64_t t_seen, t_poll, n_batches, n_polls, n_stale;
+    uint64_t t_yield;  // the leader's last look at the yield word
 };
 template <bool LEADER>
 __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc, uint32_t* s_cmd, PollState& P,
@@ -117,6 +121,15 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
             d0 = (uint64_t)d.x | ((uint64_t)d.y << 32);
             d1 = (uint64_t)d.z | ((uint64_t)d.w << 32);
         }
+    };
+    // the leader, idle: another context of the process is releasing memory the runtime will not release while any
+    // stream of the device is busy (xsk_gpu__ll_yield_all) -- leave as after an idle timeout; the next batch brings
+    // the grid back.  Looked at every kYieldTicks only: one more PCIe read.
+    auto yield_now = [&]() -> bool {
+        const uint64_t now = wall_clock64();
+        if (now - P.t_yield < kYieldTicks) return false;
+        P.t_yield = now;
+        return uniform(__hip_atomic_load((uint32_t*)L.yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
     };
     // 0: keep polling, 1: a batch for this workgroup, 2: leave
     auto examine = [&](uint64_t cv, uint64_t d0, uint64_t d1) -> int {
@@ -163,8 +176,9 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
         if (!LEADER) {  // the leader's idle exit takes every workgroup of this launch with it
             if (__hip_atomic_load(&L.diag->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L.gen)
                 return 2;
-        } else if (wall_clock64() - t0 > kIdleTicks) {
-            // leaving: clear `alive`, then look once more (the host posts, then reads `alive`)
+        } else if (wall_clock64() - t0 > kIdleTicks || yield_now()) {
+            // leaving (idle, or asked to yield the device): clear `alive`, then look once more (the host posts, then
+            // reads `alive`)
             __hip_atomic_store((uint32_t*)&bell->wg[0].alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
             const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
                                                   __HIP_MEMORY_SCOPE_SYSTEM);
@@ -397,6 +411,36 @@ static void ll_free(xsk_gpu__lowlat* ll) {
     free(ll);
 }
 
+// One yield word per device, in fine-grained host memory, allocated with the device's first channel and kept for the
+// process (freeing it would wait for the grids): every resident leader of the device reads it while idle.
+constexpr int kYieldDevs = 64;
+static pthread_mutex_t g_yield_mu = PTHREAD_MUTEX_INITIALIZER;
+static uint32_t* g_yield[kYieldDevs];
+
+static uint32_t* yield_word(int device) {
+    if (device < 0 || device >= kYieldDevs) return nullptr;
+    pthread_mutex_lock(&g_yield_mu);
+    if (!g_yield[device]) {
+        uint32_t* w = nullptr;
+        if (hipHostMalloc((void**)&w, sizeof *w, kHostFlags) == hipSuccess) {
+            __atomic_store_n(w, 0u, __ATOMIC_SEQ_CST);
+            g_yield[device] = w;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    uint32_t* w = g_yield[device];
+    pthread_mutex_unlock(&g_yield_mu);
+    return w;
+}
+
+extern "C" void xsk_gpu__ll_yield_all(int delta) {
+    pthread_mutex_lock(&g_yield_mu);
+    for (int d = 0; d < kYieldDevs; ++d)
+        if (g_yield[d]) __atomic_add_fetch(g_yield[d], (uint32_t)delta, __ATOMIC_SEQ_CST);
+    pthread_mutex_unlock(&g_yield_mu);
+}
+
 int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_size, uint32_t opts) {
     if (!out || !d_umem || (umem_size >> 48) || (opts & ~XSK_GPU_OPT_ALL)) return -EINVAL;
     *out = nullptr;
@@ -453,6 +497,11 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     A.umem_size = umem_size;
     A.opts = opts;
     A.gen = 0;
+    A.yield = yield_word(ll->device);
+    if (!A.yield) {
+        ll_free(ll);
+        return -ENOMEM;
+    }
     ll->st.bell = ll->h_bell;
     ll->st.timeout_s = 2.0;
     ll->st.quiesce_s = 1.0;
