@@ -31,6 +31,7 @@
 // so no slice is served twice.  The exit path is Dekker-safe: the leader clears `alive`, then looks at the
 // doorbell once more and resumes if a batch slipped in.
 #include <errno.h>
+#include <stddef.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -45,7 +46,13 @@ using namespace xskgpu;
 namespace {
 
 constexpr uint64_t kIdleTicks = 5000000ull;  // 50 ms at 100 MHz (s_memrealtime)
-constexpr uint64_t kYieldTicks = 4000ull;    // the leader looks at its device's yield word every 40 us while idle
+// The leader reads its channel's yield word (xsk_gpu__ll_yield_all) in the same 16-B load as the command word, so
+// looking at it costs no extra read.  XSK_LL_YIELD=0 is for the A/B of tools/ab_yield.py only: the round-5 poll (an
+// 8-B load of the command word) and no yield.
+#ifndef XSK_LL_YIELD
+#define XSK_LL_YIELD 1
+#endif
+constexpr bool kYield = XSK_LL_YIELD != 0;
 constexpr int kLLTPW = 1;                    // 16 tiles = 1024 frames per doorbell, one round
 constexpr int kLLSync = 0;                   // one round: write as soon as the wave has read
 
@@ -65,7 +72,6 @@ struct LowlatArgs {
     xsk_gpu_rec* recs;
     uint32_t opts;
     uint32_t gen;  // launch generation (the leader's exit flag names it)
-    const uint32_t* yield;  // device alias of the device's yield word (xsk_gpu__ll_yield_all): nonzero -> leave
 };
 
 __device__ __forceinline__ uint32_t ld_sys(const volatile uint32_t* p) {
@@ -82,8 +88,8 @@ __device__ __forceinline__ void st_sys(volatile uint32_t* p, uint32_t v) {
 struct PollState {
     uint32_t served;
     uint64_t cA, aA, bA, cB, aB, bB;  // the two polls' registers: they stay live across the body
+    uint32_t yA, yB;                  // the leader's: the yield word read with each command word
     uint64_t t_seen, t_poll, n_batches, n_polls, n_stale;
-    uint64_t t_yield;  // the leader's last look at the yield word
 };
 template <bool LEADER>
 __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc, uint32_t* s_cmd, PollState& P,
@@ -113,9 +119,20 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
     // the other workgroups read a line of their own, one poll at a time (their second "copy" is the
     // same word: the second read waits for the first)
     volatile uint64_t* const own = LEADER ? nullptr : &bell->wcmd[g - 1].cmd;
-    auto issue = [&](int copy, uint64_t& c, uint64_t& d0, uint64_t& d1) {
-        c = __hip_atomic_load((uint64_t*)(!LEADER ? own : copy ? &bell->cmd_b : &bell->cmd), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_SYSTEM);
+    // the leader's command word and yield word: ONE 16-B system-coherent load of the line's first 16 bytes
+    const __amdgpu_buffer_rsrc_t brs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)bell, (short)0, (int)sizeof(xsk_gpu__bell), kRsrcFlags);
+    auto issue = [&](int copy, uint64_t& c, uint64_t& d0, uint64_t& d1, uint32_t& y) {
+        if (LEADER && kYield) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                brs, copy ? (int)offsetof(xsk_gpu__bell, cmd_b) : (int)offsetof(xsk_gpu__bell, cmd), 0, kSysCoherent);
+            c = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            y = v.z;
+        } else {
+            c = __hip_atomic_load((uint64_t*)(!LEADER ? own : copy ? &bell->cmd_b : &bell->cmd), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+            y = 0u;
+        }
         if (LEADER) {
             const int dofs = (int)((copy ? XSK_GPU_LOWLAT_MAX : 0u) * sizeof(xsk_gpu_desc) + lane * 16u);
             const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(drs, dofs, 0, kSysCoherent);
@@ -123,17 +140,8 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
             d1 = (uint64_t)d.z | ((uint64_t)d.w << 32);
         }
     };
-    // the leader, idle: another context of the process is releasing memory the runtime will not release while any
-    // stream of the device is busy (xsk_gpu__ll_yield_all) -- leave as after an idle timeout; the next batch brings
-    // the grid back.  Looked at every kYieldTicks only: one more PCIe read.
-    auto yield_now = [&]() -> bool {
-        const uint64_t now = wall_clock64();
-        if (now - P.t_yield < kYieldTicks) return false;
-        P.t_yield = now;
-        return uniform(__hip_atomic_load((uint32_t*)L.yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u;
-    };
     // 0: keep polling, 1: a batch for this workgroup, 2: leave
-    auto examine = [&](uint64_t cv, uint64_t d0, uint64_t d1) -> int {
+    auto examine = [&](uint64_t cv, uint64_t d0, uint64_t d1, uint32_t y) -> int {
         ++it;
         const uint64_t c = ((uint64_t)uniform((uint32_t)(cv >> 32)) << 32) | uniform((uint32_t)cv);
         tr = (wall_clock64() - t_loop) / it;  // mean sampling interval so far
@@ -177,9 +185,9 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
         if (!LEADER) {  // the leader's idle exit takes every workgroup of this launch with it
             if (__hip_atomic_load(&L.diag->exit_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L.gen)
                 return 2;
-        } else if (wall_clock64() - t0 > kIdleTicks || yield_now()) {
-            // leaving (idle, or asked to yield the device): clear `alive`, then look once more (the host posts, then
-            // reads `alive`)
+        } else if (wall_clock64() - t0 > kIdleTicks || (kYield && uniform(y) != 0u)) {
+            // leaving -- idle, or asked to yield the device while another context unregisters host memory (the next
+            // batch brings the grid back): clear `alive`, then look once more (the host posts, then reads `alive`)
             __hip_atomic_store((uint32_t*)&bell->wg[0].alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
             const uint64_t c2 = __hip_atomic_load((uint64_t*)&bell->cmd, __ATOMIC_SEQ_CST,
                                                   __HIP_MEMORY_SCOPE_SYSTEM);
@@ -192,14 +200,14 @@ __device__ __forceinline__ void poll_doorbell(const LowlatArgs& L, u32x4* sdesc,
         }
         return 0;
     };
-    issue(0, P.cA, P.aA, P.bA);
+    issue(0, P.cA, P.aA, P.bA, P.yA);
     __builtin_amdgcn_s_sleep(22);  // ~0.6 us: half a round trip
     while (true) {
-        issue(1, P.cB, P.aB, P.bB);
-        int r = examine(P.cA, P.aA, P.bA);  // waits for A only (B is still in flight)
+        issue(1, P.cB, P.aB, P.bB, P.yB);
+        int r = examine(P.cA, P.aA, P.bA, P.yA);  // waits for A only (B is still in flight)
         if (r) break;
-        issue(0, P.cA, P.aA, P.bA);
-        r = examine(P.cB, P.aB, P.bB);
+        issue(0, P.cA, P.aA, P.bA, P.yA);
+        r = examine(P.cB, P.aB, P.bB, P.yB);
         if (r) break;
     }
     // ONE system-scope acquire for the workgroup: fresh descriptors and frames.  The doorbell read it
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(kThreads6, 1) void lowlat_kernel(LowlatArgs L) {
                                                                                                           ntiles, sm);
         // the two polls' registers live across the body: a batch is taken while the other poll is still in
         // flight, and registers the compiler reused would first have to wait for it to land
-        asm volatile("" ::"v"(P.cA), "v"(P.aA), "v"(P.bA), "v"(P.cB), "v"(P.aB), "v"(P.bB));
+        asm volatile("" ::"v"(P.cA), "v"(P.aA), "v"(P.bA), "v"(P.cB), "v"(P.aB), "v"(P.bB), "v"(P.yA), "v"(P.yB));
         const uint64_t t_rel = wall_clock64();
         const uint64_t c_rel = __builtin_amdgcn_s_memtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have reached the L2 / fabric
@@ -333,6 +341,8 @@ struct xsk_gpu__lowlat {
     uint64_t host_ns[2];   // last batch on the host: entry -> doorbell posted, posted -> completion seen
     double h_enter, h_post; // the batch in flight: entry, doorbell posted
     uint32_t width;        // workgroups a launch starts (0: XSK_GPU__LL_WG); xsk_gpu__lowlat_test_width
+    xsk_gpu__lowlat* next; // the live channels (xsk_gpu__ll_yield_all)
+    int listed;
 };
 
 static int ll_launch(void* u) {
@@ -391,6 +401,17 @@ int xsk_gpu__lowlat_recover(xsk_gpu__lowlat* ll) {
     return 1;
 }
 
+// The live channels of the process and the yield requests in force (xsk_gpu__ll_yield_all): a channel's yield words
+// hold the count, set when the channel starts and whenever the count changes.
+static pthread_mutex_t g_yield_mu = PTHREAD_MUTEX_INITIALIZER;
+static xsk_gpu__lowlat* g_chans;
+static uint32_t g_yield_req;
+
+static void set_yield(xsk_gpu__lowlat* ll, uint32_t v) {
+    __atomic_store_n(&ll->h_bell->yield, v, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&ll->h_bell->yield_b, v, __ATOMIC_SEQ_CST);
+}
+
 // the channel's pinned host buffers: fine-grained (coherent) and mapped, so no GPU cache ever holds a copy
 constexpr unsigned kHostFlags = hipHostMallocMapped | hipHostMallocCoherent;
 constexpr size_t kDescBytes = (size_t)(XSK_GPU_LOWLAT_MAX + 64u) * sizeof(struct xsk_gpu_desc);
@@ -398,6 +419,16 @@ constexpr size_t kRecBytes = (size_t)XSK_GPU_LOWLAT_MAX * sizeof(struct xsk_gpu_
 
 static void ll_free(xsk_gpu__lowlat* ll) {
     if (!ll) return;
+    if (ll->listed) {  // no yield request writes to this channel's bell from here on
+        pthread_mutex_lock(&g_yield_mu);
+        for (xsk_gpu__lowlat** p = &g_chans; *p; p = &(*p)->next)
+            if (*p == ll) {
+                *p = ll->next;
+                break;
+            }
+        pthread_mutex_unlock(&g_yield_mu);
+        ll->listed = 0;
+    }
     xsk_gpu__lowlat_stop(ll);
     if (ll->stream) (void)hipStreamDestroy(ll->stream);
     // kept for the next channel while another resident grid runs on the device (xsk_gpu__buf_free: the runtime's
@@ -412,33 +443,10 @@ static void ll_free(xsk_gpu__lowlat* ll) {
     free(ll);
 }
 
-// One yield word per device, in fine-grained host memory, allocated with the device's first channel and kept for the
-// process (freeing it would wait for the grids): every resident leader of the device reads it while idle.
-constexpr int kYieldDevs = 64;
-static pthread_mutex_t g_yield_mu = PTHREAD_MUTEX_INITIALIZER;
-static uint32_t* g_yield[kYieldDevs];
-
-static uint32_t* yield_word(int device) {
-    if (device < 0 || device >= kYieldDevs) return nullptr;
-    pthread_mutex_lock(&g_yield_mu);
-    if (!g_yield[device]) {
-        uint32_t* w = nullptr;
-        if (hipHostMalloc((void**)&w, sizeof *w, kHostFlags) == hipSuccess) {
-            __atomic_store_n(w, 0u, __ATOMIC_SEQ_CST);
-            g_yield[device] = w;
-        } else {
-            (void)hipGetLastError();
-        }
-    }
-    uint32_t* w = g_yield[device];
-    pthread_mutex_unlock(&g_yield_mu);
-    return w;
-}
-
 extern "C" void xsk_gpu__ll_yield_all(int delta) {
     pthread_mutex_lock(&g_yield_mu);
-    for (int d = 0; d < kYieldDevs; ++d)
-        if (g_yield[d]) __atomic_add_fetch(g_yield[d], (uint32_t)delta, __ATOMIC_SEQ_CST);
+    g_yield_req += (uint32_t)delta;
+    for (xsk_gpu__lowlat* c = g_chans; c; c = c->next) set_yield(c, g_yield_req);
     pthread_mutex_unlock(&g_yield_mu);
 }
 
@@ -498,11 +506,12 @@ int xsk_gpu__lowlat_start(xsk_gpu__lowlat** out, void* d_umem, uint64_t umem_siz
     A.umem_size = umem_size;
     A.opts = opts;
     A.gen = 0;
-    A.yield = yield_word(ll->device);
-    if (!A.yield) {
-        ll_free(ll);
-        return -ENOMEM;
-    }
+    pthread_mutex_lock(&g_yield_mu);  // a live channel from here on: its yield words follow the requests
+    set_yield(ll, g_yield_req);
+    ll->next = g_chans;
+    g_chans = ll;
+    ll->listed = 1;
+    pthread_mutex_unlock(&g_yield_mu);
     ll->st.bell = ll->h_bell;
     ll->st.timeout_s = 2.0;
     ll->st.quiesce_s = 1.0;

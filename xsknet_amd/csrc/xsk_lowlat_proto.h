@@ -43,11 +43,16 @@ struct xsk_gpu__bell {
      *   bits 56-58 workgroups serving the batch (1..XSK_GPU__LL_WG), bit 63 stop (every workgroup exits at
      *   its next poll) */
     volatile uint64_t cmd;
-    uint32_t pad0[14];
-    /* the same word again in a line of its own: the leader keeps two polls in flight, one per copy (two
+    /* nonzero while another context of the process unregisters host memory (the runtime then waits for every stream
+     * of the device): the leader reads it with `cmd` in one 16-B load and, idle, leaves (xsk_gpu__ll_yield_all).
+     * Written by whichever thread raises or drops the request, never by the channel's owner. */
+    volatile uint32_t yield;
+    uint32_t pad0[13];
+    /* the same words again in a line of their own: the leader keeps two polls in flight, one per copy (two
      * reads of ONE line do not overlap -- the second waits for the first) */
     volatile uint64_t cmd_b;
-    uint32_t pad0b[14];
+    volatile uint32_t yield_b;
+    uint32_t pad0b[13];
     /* the same word once more for each other workgroup, a line each: reads of one host line from several CUs
      * queue behind each other, so workgroups polling the leader's lines slowed its sampling of the doorbell
      * from every ~0.7 us to every ~1.0-1.6 us */
