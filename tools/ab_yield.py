@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "xsknet_amd", "csrc")
 OUT = os.path.join(ROOT, "tools", "ab_yield")
 POLICIES = (0, 1)
-RUNS = (("step64", ["64"], []), ("step64_pipe4", ["64"], ["pipe=4"]), ("step1024", ["1024"], []))
+RUNS = (("step64", ["64"], [], {}), ("step64_pipe4", ["64"], ["pipe=4"], {}), ("step1024", ["1024"], [], {}),
+        ("step64_pipe8_hwq8", ["64"], ["pipe=8"], {"GPU_MAX_HW_QUEUES": "8"}))
 
 
 def build():
@@ -41,7 +42,7 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=2.0)
-    ap.add_argument("--runs", default="step64,step64_pipe4,step1024")
+    ap.add_argument("--runs", default="step64,step64_pipe4,step1024,step64_pipe8_hwq8")
     args = ap.parse_args()
     if args.build:
         build()
@@ -50,8 +51,8 @@ def main():
     res = {}
     for rnd in range(args.rounds):
         for pol in POLICIES:
-            env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(OUT, f"v{pol}"))
-            for name, step, extra in [r for r in RUNS if r[0] in args.runs.split(",")]:
+            for name, step, extra, xenv in [r for r in RUNS if r[0] in args.runs.split(",")]:
+                env = dict(os.environ, LD_LIBRARY_PATH=os.path.join(OUT, f"v{pol}"), **xenv)
                 cmd = [exe] + step + ["lowlat", str(args.seconds), "len=64", "huge=1", "ring=16384", "frames=16384",
                                       "nic=burst"] + extra
                 r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env)
