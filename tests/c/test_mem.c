@@ -95,8 +95,9 @@ hipError_t hipHostFree(void* p) {
     return hipSuccess;
 }
 
-static atomic_int g_yield_requests, g_yield_max;
+static atomic_int g_yield_requests, g_yield_max, g_yield_raises;
 void xsk_gpu__ll_yield_all(int delta) {
+    if (delta > 0) atomic_fetch_add(&g_yield_raises, 1);
     const int v = atomic_fetch_add(&g_yield_requests, delta) + delta;
     assert(v >= 0);
     int m = atomic_load(&g_yield_max);
@@ -170,13 +171,17 @@ static void test_buffers(void) {
     void* g[3];
     for (int i = 0; i < 3; i++) assert(xsk_gpu__buf_alloc(0, XSK_GPU__BUF_DEV, &g[i], 3ull << 30) == hipSuccess);
     const long d0 = live_dev;
+    const int r0 = g_yield_raises;
     for (int i = 0; i < 3; i++) xsk_gpu__buf_free(0, XSK_GPU__BUF_DEV, g[i], 3ull << 30);
     assert(xsk_gpu__buf_kept(0) == 4 && live_dev == d0 - 1);
+    assert(g_yield_raises == r0 + 1 && g_yield_requests == 0); /* the one free while busy asked the grids aside */
     /* the count limit */
     static void* s[POOL_MAX + 8];
     for (int i = 0; i < POOL_MAX + 8; i++) assert(xsk_gpu__buf_alloc(0, XSK_GPU__BUF_DEV, &s[i], 64) == hipSuccess);
+    const int r1 = g_yield_raises;
     for (int i = 0; i < POOL_MAX + 8; i++) xsk_gpu__buf_free(0, XSK_GPU__BUF_DEV, s[i], 64);
     assert(xsk_gpu__buf_kept(0) == POOL_MAX);
+    assert(g_yield_raises == r1 + 12 && g_yield_requests == 0); /* 4 kept before + 256 limit: 12 frees past it */
     /* idle again: the next release (or the drain every fini ends with) frees everything kept */
     atomic_store(&g_busy[0], 0);
     xsk_gpu__buf_free(0, 0, NULL, 0);

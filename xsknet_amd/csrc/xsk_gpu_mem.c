@@ -114,7 +114,8 @@ int xsk_gpu__umem_refs(const void* base) {
  * leaves its stream only when it stops or has idled 50 ms (tools/fini_block.py, profiles/r06/fini_block.jsonl: 2.5 s
  * beside a busy grid).  So a buffer released while any LOWLAT slot of its device is taken is kept here instead, for
  * the next allocation of the same device, kind and size; kept buffers are freed once no slot of the device is taken
- * (xsk_gpu__buf_free(d, 0, NULL, 0) at the end of every fini).  With the UMEM registration shared (xsk_gpu__umem_ref),
+ * (xsk_gpu__buf_free(d, 0, NULL, 0) at the end of every fini).  Past 256 buffers or 8 GiB a release frees at once,
+ * with the resident grids asked to step aside (xsk_gpu__ll_yield_all) for the runtime's wait.  With the UMEM registration shared (xsk_gpu__umem_ref),
  * closing one RX queue's context beside another queue's busy LOWLAT context then waits for nothing.  `kind`:
  * XSK_GPU__BUF_DEV (hipMalloc) or XSK_GPU__BUF_HOST | hipHostMalloc flags.  A reused host buffer is zeroed as a fresh
  * one's pages are; device buffers carry no such promise either way. */
@@ -160,7 +161,7 @@ void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size) {
         void* p;
         unsigned kind;
     } drop[POOL_MAX + 1];
-    int ndrop = 0;
+    int ndrop = 0, busy = 0;
     pthread_mutex_lock(&g_pool_mu);
     if (!xsk_gpu__ll_busy(device)) { /* no resident grid: free it, and whatever was kept for this device */
         for (int i = 0; i < g_npool;)
@@ -183,12 +184,15 @@ void xsk_gpu__buf_free(int device, unsigned kind, void* p, size_t size) {
         g_pool[g_npool].device = device;
         g_pool[g_npool].kind = kind;
         g_npool++;
-    } else if (p) { /* the pool is full (entries or bytes): free it (and wait) */
+    } else if (p) { /* the pool is full (entries or bytes): free it, the resident grids asked to step aside */
         drop[ndrop].p = p;
         drop[ndrop++].kind = kind;
+        busy = 1;
     }
     pthread_mutex_unlock(&g_pool_mu);
+    if (busy) xsk_gpu__ll_yield_all(+1);
     for (int i = 0; i < ndrop; i++) buf_release(drop[i].kind, drop[i].p);
+    if (busy) xsk_gpu__ll_yield_all(-1);
 }
 
 int xsk_gpu__buf_kept(int device) {
