@@ -236,8 +236,8 @@ int xsk_gpu_lowlat_cap(int device);
  * runtime (hipHostRegister, portable + mapped) until the last context, multi object or pipe over it is released:
  * several of them may share one UMEM (AF_XDP sockets sharing a UMEM, one context per RX queue), and the library counts
  * its users of each registration (the runtime keeps one per base and does not); a UMEM that is a part of one already
- * registered by the library uses that registration.  -EBUSY for a UMEM that starts inside such a registration and
- * runs past its end.  A UMEM the caller registered with the runtime itself is used as it is (it must be mapped) and
+ * registered by the library uses that registration.  -EBUSY for a UMEM that overlaps such a registration without
+ * lying inside it (no two registrations ever share a page).  A UMEM the caller registered with the runtime itself is used as it is (it must be mapped) and
  * stays registered.  max_batch bounds n of later calls. */
 int xsk_gpu_init(xsk_gpu_ctx** out, int device, void* umem, uint64_t umem_size, uint32_t max_batch, int mode);
 

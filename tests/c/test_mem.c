@@ -4,7 +4,7 @@
  * registration per base address, a second hipHostRegister of a registered base a silent success, the first
  * hipHostUnregister removing it, hipPointerGetAttributes reporting any address inside a registration as host memory.
  * Checked: one runtime registration per UMEM however many users, parts of a UMEM sharing its registration, -EBUSY for
- * a range running past one, a caller's own registration left alone, the table's limit; buffers kept only while the
+ * a range overlapping one without lying inside it, a caller's own registration left alone, the table's limit; buffers kept only while the
  * device is busy, reused by exact (device, kind, size), host ones zeroed on reuse, the 256-buffer and 8-GiB limits,
  * everything freed once the device is idle; and, on 8 threads, that no user ever finds its UMEM unregistered while it
  * holds a reference and that every registration and buffer is released at the end.
@@ -127,6 +127,15 @@ static void test_registrations(void) {
     assert(!rt_covers(u, 1) && rt_unregisters == u0 + 1 && xsk_gpu__umem_refs(u) == 0);
     assert(g_yield_requests == 0 && g_yield_max == 1); /* grids asked to yield around the unregistration only */
     xsk_gpu__umem_unref(NULL); /* no-op */
+
+    static uint8_t w[96 * 4096] __attribute__((aligned(4096)));
+    void* rw = NULL;
+    assert(xsk_gpu__umem_ref(w + 16 * 4096, 32 * 4096, &rw) == 0 && rw == w + 16 * 4096);
+    assert(xsk_gpu__umem_ref(w, 32 * 4096, &rd) == -EBUSY && rd == NULL);          /* runs into it from below */
+    assert(xsk_gpu__umem_ref(w, sizeof w, &rd) == -EBUSY && rd == NULL);           /* covers it */
+    assert(xsk_gpu__umem_ref(w, 16 * 4096, &rd) == 0 && rd == w);                  /* ends where it starts */
+    xsk_gpu__umem_unref(rd);
+    xsk_gpu__umem_unref(rw);
 
     /* a caller's own registration: used, left registered */
     assert(hipHostRegister(u, sizeof u, 0) == hipSuccess);

@@ -300,10 +300,10 @@ def test_contexts_sharing_one_umem(mode):
     removes it for both -- so when one of two contexts over one UMEM (AF_XDP sockets sharing a UMEM, one context per RX
     queue) closed, the other went on over a UMEM the runtime no longer held registered, and a UMEM the caller had
     registered itself lost its registration at the library's close.  The library now counts its users of each
-    registration (xsk_gpu__umem_ref).  Checked: two contexts, a context over a part of the UMEM, a multi object and a pipe over one
-    UMEM serve their shares exactly; after any of them closes the others still serve exactly; a UMEM that starts inside
-    a registration and runs past its end gets -EBUSY; the last close releases the registration; a UMEM the caller
-    registered itself stays registered."""
+    registration (xsk_gpu__umem_ref).  Checked: two contexts, a context over a part of the UMEM, a multi object and a
+    pipe over one UMEM serve their shares exactly; after any of them closes the others still serve exactly; a UMEM
+    that overlaps a registration without lying inside it gets -EBUSY; the last close releases the registration; a
+    UMEM the caller registered itself stays registered."""
     _dev()
     n = 2048
     req = np.zeros(n * 4096, np.uint8)
@@ -326,7 +326,7 @@ def test_contexts_sharing_one_umem(mode):
         serve(a, slice(0, n, 2))  # queue 0: even frames
         serve(b, slice(1, n, 2))  # queue 1: odd frames
         assert (u == ref).all()
-        with pytest.raises(X.XskGpuError, match="EBUSY"):  # more bytes than the registration of this base covers
+        with pytest.raises(X.XskGpuError, match="EBUSY"):  # overlaps the registration without lying inside it
             X.EchoContext(big, 0, max_batch=64, mode=mode)
         assert refs() == 2
         b.close()

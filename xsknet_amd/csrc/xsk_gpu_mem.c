@@ -20,8 +20,9 @@
  * on over a UMEM the runtime no longer held registered, and a registration the caller had made was removed by the
  * library's close.  Every registration the library makes goes through this table: the first user of a base
  * registers it (portable + mapped), later users of the same UMEM -- or of a part of it -- take a reference of that
- * registration, the last one unregisters.  A UMEM that starts inside a registration and runs past its end gets
- * -EBUSY.  A base the runtime already knows as host memory and that lies in none of the library's registrations (the
+ * registration, the last one unregisters.  A UMEM that overlaps a registration without lying inside it gets -EBUSY:
+ * the library never makes two registrations that share a page (round 5's failures all ran on such layouts, DESIGN.md
+ * §5).  A base the runtime already knows as host memory and that lies in none of the library's registrations (the
  * caller registered it) is used and never unregistered here.  The lock is held across the runtime calls, so a
  * concurrent user of the same base never sees it half registered or half released. */
 #define UMEM_REG_MAX 256
@@ -46,7 +47,7 @@ int xsk_gpu__umem_ref(void* base, uint64_t size, void** reg_base) {
             *reg_base = g_reg[i].base;
             goto out;
         }
-        if (elo <= lo && lo < ehi) { /* starts inside a registration and runs past its end */
+        if (lo < ehi && elo < hi) { /* overlaps a registration without lying inside it */
             rc = -EBUSY;
             goto out;
         }
