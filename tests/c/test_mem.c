@@ -1,14 +1,14 @@
-/* CPU unit test of the host memory bookkeeping (xsknet_amd/csrc/xsk_gpu_mem.c): the counted table of UMEM
- * registrations and the buffers kept for reuse while a resident LOWLAT grid runs.  The HIP runtime calls are stubs that
- * behave as the runtime was measured to (tools/doublereg_probe.py, profiles/r06/doublereg_attributes.jsonl): one
- * registration per base address, a second hipHostRegister of a registered base a silent success, the first
- * hipHostUnregister removing it, hipPointerGetAttributes reporting any address inside a registration as host memory.
- * Checked: one runtime registration per UMEM however many users, parts of a UMEM sharing its registration, -EBUSY for
- * a range overlapping one without lying inside it, a caller's own registration left alone, the table's limit; buffers kept only while the
+/* CPU unit test of the host memory bookkeeping (xsknet_amd/csrc/xsk_gpu_mem.c): the counted table of UMEM registrations
+ * and the buffers kept for reuse while a resident LOWLAT grid runs. The HIP runtime calls are stubs that behave as the
+ * runtime was measured to (tools/doublereg_probe.py, profiles/r06/doublereg_attributes.jsonl): one registration per
+ * base address, a second hipHostRegister of a registered base a silent success, the first hipHostUnregister removing
+ * it, hipPointerGetAttributes reporting any address inside a registration as host memory. Checked: one runtime
+ * registration per UMEM however many users, parts of a UMEM sharing its registration, -EBUSY for a range overlapping
+ * one without lying inside it, a caller's own registration left alone, the table's limit; buffers kept only while the
  * device is busy, reused by exact (device, kind, size), host ones zeroed on reuse, the 256-buffer and 8-GiB limits,
  * everything freed once the device is idle; and, on 8 threads, that no user ever finds its UMEM unregistered while it
- * holds a reference and that every registration and buffer is released at the end.
- * Built and run by tests/test_mem_c.py. */
+ * holds a reference and that every registration and buffer is released at the end. Built and run by
+ * tests/test_mem_c.py. */
 #include <assert.h>
 #include <pthread.h>
 #include <stdatomic.h>

@@ -110,16 +110,16 @@ int xsk_gpu__umem_refs(const void* base) {
     return n;
 }
 
-/* Buffers of contexts and LOWLAT channels (round 6).  The HIP runtime's hipFree, and its hipHostFree of pinned memory a
- * kernel has used, wait for every stream of the device -- another context's resident LOWLAT grid included, which
- * leaves its stream only when it stops or has idled 50 ms (tools/fini_block.py, profiles/r06/fini_block.jsonl: 2.5 s
- * beside a busy grid).  So a buffer released while any LOWLAT slot of its device is taken is kept here instead, for
- * the next allocation of the same device, kind and size; kept buffers are freed once no slot of the device is taken
- * (xsk_gpu__buf_free(d, 0, NULL, 0) at the end of every fini).  Past 256 buffers or 8 GiB a release frees at once,
- * with the resident grids asked to step aside (xsk_gpu__ll_yield_all) for the runtime's wait.  With the UMEM registration shared (xsk_gpu__umem_ref),
- * closing one RX queue's context beside another queue's busy LOWLAT context then waits for nothing.  `kind`:
- * XSK_GPU__BUF_DEV (hipMalloc) or XSK_GPU__BUF_HOST | hipHostMalloc flags.  A reused host buffer is zeroed as a fresh
- * one's pages are; device buffers carry no such promise either way. */
+/* Buffers of contexts and LOWLAT channels (round 6). The HIP runtime's hipFree, and its hipHostFree of pinned memory a
+ * kernel has used, wait for every stream of the device -- another context's resident LOWLAT grid included, which leaves
+ * its stream only when it stops or has idled 50 ms (tools/fini_block.py, profiles/r06/fini_block.jsonl: 2.5 s beside a
+ * busy grid). So a buffer released while any LOWLAT slot of its device is taken is kept here instead, for the next
+ * allocation of the same device, kind and size; kept buffers are freed once no slot of the device is taken
+ * (xsk_gpu__buf_free(d, 0, NULL, 0) at the end of every fini). Past 256 buffers or 8 GiB a release frees at once, with
+ * the resident grids asked to step aside (xsk_gpu__ll_yield_all) for the runtime's wait. With the UMEM registration
+ * shared (xsk_gpu__umem_ref), closing one RX queue's context beside another queue's busy LOWLAT context then waits for
+ * nothing. `kind`: XSK_GPU__BUF_DEV (hipMalloc) or XSK_GPU__BUF_HOST | hipHostMalloc flags. A reused host buffer is
+ * zeroed as a fresh one's pages are; device buffers carry no such promise either way. */
 #define POOL_MAX 256
 #define POOL_BYTES_MAX (8ull << 30) /* kept at most, over every device and kind (a STAGED mirror is the UMEM's size) */
 static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;

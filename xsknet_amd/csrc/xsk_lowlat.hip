@@ -22,14 +22,14 @@
 // issues ONE system-scope release fence (the L2 write-back covers every wave's stores to the UMEM,
 // verdicts and records), waits for the write-back, and stores the batch's sequence number to its `done`.
 //
-// Exit conditions every wave reaches: the host's stop word, or no batch for kIdleTicks (50 ms of the
-// 100-MHz wall clock) at the leader -- or, idle, its channel's yield word raised (another context is about to unregister
-// host memory, which waits for every stream of the device) -- whose exit flag (device memory, tagged with the launch generation)
-// the other workgroups poll — so a process that dies without xsk_gpu_fini() never leaves the grid running.
-// The host relaunches the grid lazily when it finds the leader gone (alive == 0 before posting, or the
-// kernel's stream idle while a batch waits); a relaunched workgroup takes its baseline from its own `done`,
-// so no slice is served twice.  The exit path is Dekker-safe: the leader clears `alive`, then looks at the
-// doorbell once more and resumes if a batch slipped in.
+// Exit conditions every wave reaches: the host's stop word, or no batch for kIdleTicks (50 ms of the 100-MHz wall
+// clock) at the leader -- or, idle, its channel's yield word raised (another context is about to unregister host
+// memory, which waits for every stream of the device) -- whose exit flag (device memory, tagged with the launch
+// generation) the other workgroups poll — so a process that dies without xsk_gpu_fini() never leaves the grid running.
+// The host relaunches the grid lazily when it finds the leader gone (alive == 0 before posting, or the kernel's stream
+// idle while a batch waits); a relaunched workgroup takes its baseline from its own `done`, so no slice is served
+// twice. The exit path is Dekker-safe: the leader clears `alive`, then looks at the doorbell once more and resumes if a
+// batch slipped in.
 #include <errno.h>
 #include <stddef.h>
 #include <pthread.h>
